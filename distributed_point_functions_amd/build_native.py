@@ -1,0 +1,123 @@
+"""Builds the native pieces in-tree (no JIT cache, so they travel to the GPU box).
+
+* ``distributed_point_functions_amd/lib/libdpf_hip.so`` -- HIP kernels + the C ABI
+  of ``include/dpf_hip.h`` (hipcc, ``--offload-arch=gfx950``).
+* ``distributed_point_functions_amd/lib/libdpf.so`` -- the host C++
+  ``DistributedPointFunction`` (reference API) on top of that C ABI.
+* ``distributed_point_functions_amd/lib/_dpf_host*.so`` -- pybind11 module over
+  the host library (Python mirror used by tests and bench).
+* ``oracle/liboracle_dpf.so`` -- the CPU parity oracle (test infrastructure).
+
+Usage: ``python -m distributed_point_functions_amd.build_native [--only hip|host|oracle]``
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "distributed_point_functions_amd")
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+INCLUDE = os.path.join(ROOT, "include")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+HIPCC = os.path.join(ROCM, "bin", "hipcc")
+
+HIP_FLAGS = [
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-mcode-object-version=5", "-Wall", "-Wno-unused-function",
+]
+
+
+def _run(cmd, cwd=ROOT):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, cwd=cwd, check=True)
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _files(d, exts):
+    res = []
+    for root, _, fs in os.walk(d):
+        for f in fs:
+            if f.endswith(exts):
+                res.append(os.path.join(root, f))
+    return res
+
+
+def build_hip(force=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, "libdpf_hip.so")
+    src = os.path.join(CSRC, "kernels", "dpf_kernels.hip")
+    deps = _files(os.path.join(CSRC, "kernels"), (".hip", ".h")) + [os.path.join(INCLUDE, "dpf_hip.h")]
+    if force or _stale(out, deps):
+        _run([HIPCC, *HIP_FLAGS, f"-I{INCLUDE}", src, "-o", out])
+    return out
+
+
+def build_host(force=False):
+    """Host C++ library (reference API) + pybind11 module."""
+    host_dir = os.path.join(CSRC, "host")
+    srcs = sorted(f for f in _files(host_dir, (".cc",)) if not f.endswith("_pybind.cc"))
+    if not srcs:
+        return None
+    os.makedirs(LIBDIR, exist_ok=True)
+    hdrs = _files(os.path.join(INCLUDE), (".h",)) + _files(host_dir, (".h",))
+    out = os.path.join(LIBDIR, "libdpf.so")
+    cxx = os.environ.get("CXX", "g++")
+    common = ["-O2", "-std=c++20", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+              "-maes", "-msse4.1", f"-I{INCLUDE}"]
+    if force or _stale(out, srcs + hdrs + [os.path.join(LIBDIR, "libdpf_hip.so")]):
+        _run([cxx, *common, "-shared", *srcs, "-o", out, f"-L{LIBDIR}", "-ldpf_hip",
+              "-Wl,-rpath,$ORIGIN"])
+    pyb = os.path.join(host_dir, "dpf_pybind.cc")
+    if os.path.exists(pyb):
+        import pybind11
+        suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+        mod = os.path.join(LIBDIR, "_dpf_host" + suffix)
+        if force or _stale(mod, [pyb, out] + hdrs):
+            _run([cxx, *common, "-shared", pyb, "-o", mod,
+                  f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+                  f"-L{LIBDIR}", "-ldpf", "-ldpf_hip", "-Wl,-rpath,$ORIGIN"])
+    return out
+
+
+def build_oracle(force=False):
+    odir = os.path.join(ROOT, "oracle")
+    out = os.path.join(odir, "liboracle_dpf.so")
+    if force or _stale(out, [os.path.join(odir, "dpf_oracle.c")]):
+        _run(["make", "-C", odir, "-B" if force else "liboracle_dpf.so"])
+    return out
+
+
+def build_all(force=False):
+    build_hip(force)
+    build_host(force)
+    build_oracle(force)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", choices=["hip", "host", "oracle"])
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args(argv)
+    if a.only == "hip":
+        build_hip(a.force)
+    elif a.only == "host":
+        build_host(a.force)
+    elif a.only == "oracle":
+        build_oracle(a.force)
+    else:
+        build_all(a.force)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

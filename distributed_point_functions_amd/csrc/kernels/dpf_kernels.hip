@@ -1,0 +1,1021 @@
+// dpf_kernels.hip -- MI355X (gfx950) kernels for incremental-DPF evaluation and
+// the C ABI declared in include/dpf_hip.h.
+//
+// Hot path:
+//   * AES-128 MMO hash with the four T-tables replicated 32x across LDS banks
+//     (128 KiB): lane l reads copy (l & 31), so every ds_read_b32 of a wave is
+//     bank-conflict-free whatever the table index.  3-input XORs are single
+//     v_bitop3_b32 (gfx950).  One 1024-thread workgroup per CU.
+//   * expand_kernel: one thread = one subtree.  It walks from its start seed to
+//     the subtree root along the bits of its work-item index (per-lane key
+//     select), then visits the subtree depth-first with the path stack held in
+//     VGPRs (uniform control flow: every lane of a wave is at the same leaf
+//     pair), hashing each leaf with the value key, converting, correcting and
+//     storing it.  Intermediate seeds never touch HBM; only leaves are written.
+//   * eval_points_kernel: one thread = one (key, point) path walk, fused with the
+//     leaf hash, conversion, correction and the store of the selected element.
+//   * Correction words live in LDS (broadcast reads).
+// All arithmetic is integer/bitwise; no MFMA (nothing here is a contraction).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../../include/dpf_hip.h"
+#include "aes_core.h"
+
+namespace {
+
+// ------------------------------------------------------------------------
+// Status plumbing (absl codes)
+// ------------------------------------------------------------------------
+constexpr int kOk = 0, kInvalidArgument = 3, kResourceExhausted = 8, kUnimplemented = 12,
+              kInternal = 13;
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? kResourceExhausted : kInternal,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t _e = (expr);                             \
+    if (_e != hipSuccess) return hip_fail(_e, #expr);   \
+  } while (0)
+
+// ------------------------------------------------------------------------
+// Tables and keys
+// ------------------------------------------------------------------------
+struct T0Table {
+  uint32_t v[256];
+};
+constexpr T0Table make_t0() {
+  T0Table t{};
+  for (int i = 0; i < 256; ++i) {
+    uint32_t s = dpf_aes::kSbox[i];
+    uint32_t s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
+    t.v[i] = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
+  }
+  return t;
+}
+__constant__ T0Table c_t0 = make_t0();
+
+struct RoundKeys {
+  uint32_t k[44];
+};
+
+RoundKeys expand_key(const dpf_aes_key* key) {
+  RoundKeys rk;
+  dpf_aes::expand_key(key->bytes, rk.k);
+  return rk;
+}
+
+constexpr int kBlock = 1024;             // threads per workgroup (16 waves)
+constexpr int kTabWords = 4 * 256 * 32;  // 4 tables x 256 entries x 32 bank copies = 128 KiB
+constexpr int kMaxCwLevels = 128;
+constexpr int kSMax = 12;                // max subtree depth handled per thread
+constexpr int kGMax = kSMax - 1;         // max depth of the DFS stack above leaf pairs
+constexpr int kBMax = 8;                 // max AES blocks hashed per leaf (generic path)
+
+// LDS image: [tables 128 KiB][cw seeds 128 x 16 B][cw control 128 x 4 B]
+struct LdsImage {
+  uint32_t tab[kTabWords];
+  uint4 cw_seed[kMaxCwLevels];
+  uint32_t cw_ctrl[kMaxCwLevels];
+};
+
+__device__ __forceinline__ void fill_tables(uint32_t* tab) {
+  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) {
+    int t = i >> 13, e = (i >> 5) & 255;
+    uint32_t v = c_t0.v[e];
+    tab[i] = t == 0 ? v : ((v << (8 * t)) | (v >> (32 - 8 * t)));
+  }
+}
+
+__device__ __forceinline__ void fill_cws(LdsImage& lds, const dpf_block* cw_seed,
+                                         const uint8_t* cw_left, const uint8_t* cw_right,
+                                         int num_levels) {
+  for (int i = threadIdx.x; i < num_levels; i += blockDim.x) {
+    dpf_block b = cw_seed[i];
+    lds.cw_seed[i] = make_uint4((uint32_t)b.low, (uint32_t)(b.low >> 32), (uint32_t)b.high,
+                                (uint32_t)(b.high >> 32));
+    lds.cw_ctrl[i] = (uint32_t)(cw_left[i] & 1) | ((uint32_t)(cw_right[i] & 1) << 1);
+  }
+}
+
+// Conflict-free LDS T-table lookups: byte K of w selects entry, copy = lane & 31.
+struct LdsLookup {
+  const char* base;
+  uint32_t l0;  // (lane & 31) * 4
+  uint32_t l2;  // (lane & 31) * 4 + 65536 (tables 2 and 3)
+  template <int T, int K>
+  __device__ __forceinline__ uint32_t lookup(uint32_t w) const {
+    uint32_t idx;
+    if (K == 0) idx = (w << 7) & 0x7f80u;
+    else if (K == 1) idx = (w >> 1) & 0x7f80u;
+    else if (K == 2) idx = (w >> 9) & 0x7f80u;
+    else idx = (w >> 17) & 0x7f80u;
+    uint32_t off = (idx | (T < 2 ? l0 : l2)) + ((T & 1) ? 32768u : 0u);
+    return *reinterpret_cast<const uint32_t*>(base + off);
+  }
+  __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) const {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+  }
+};
+
+__device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds) {
+  uint32_t lane = threadIdx.x & 31;
+  return LdsLookup{reinterpret_cast<const char*>(lds.tab), lane * 4u, lane * 4u + 65536u};
+}
+
+// Round keys shared by the whole wave (kernel-argument resident).
+struct UniformRK {
+  const uint32_t* k;
+  __device__ __forceinline__ uint32_t operator()(int i) const { return k[i]; }
+};
+// Per-lane key choice: rk = left ^ (mask & (left ^ right)).
+struct SelectRK {
+  const uint32_t* left;
+  const uint32_t* diff;
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t operator()(int i) const { return left[i] ^ (mask & diff[i]); }
+};
+
+using dpf_aes::Block4;
+
+__device__ __forceinline__ Block4 load_block(const dpf_block* p) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  return Block4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void store_block(dpf_block* p, Block4 b) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(b.w0, b.w1, b.w2, b.w3);
+}
+__device__ __forceinline__ Block4 add_small(Block4 s, uint32_t j) {
+  // seed + j as absl::uint128 (distributed_point_function.cc:512)
+  uint64_t lo = ((uint64_t)s.w1 << 32) | s.w0, hi = ((uint64_t)s.w3 << 32) | s.w2;
+  uint64_t nlo = lo + j;
+  hi += (nlo < lo) ? 1 : 0;
+  return Block4{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// One tree step for a uniformly chosen child: seed/control correction and
+// control-bit extraction in the order of distributed_point_function.cc:323-343.
+__device__ __forceinline__ void child_step(const LdsLookup& lk, const uint32_t* rk, Block4 s,
+                                           uint32_t t, uint32_t dir, uint4 cs, uint32_t cctl,
+                                           Block4& out, uint32_t& tout) {
+  Block4 h = dpf_aes::mmo_hash(s, lk, UniformRK{rk});
+  uint32_t m = 0u - t;
+  h.w0 ^= cs.x & m; h.w1 ^= cs.y & m; h.w2 ^= cs.z & m; h.w3 ^= cs.w & m;
+  uint32_t nt = h.w0 & 1u;
+  h.w0 &= ~1u;
+  nt ^= t & ((cctl >> dir) & 1u);
+  out = h;
+  tout = nt;
+}
+
+// Path step with a per-lane direction bit (evaluate_prg_hwy.cc:452-486).
+__device__ __forceinline__ void path_step(const LdsLookup& lk, const RoundKeys& rkl,
+                                          const RoundKeys& rkd, Block4& s, uint32_t& t,
+                                          uint32_t bit, uint4 cs, uint32_t cctl) {
+  Block4 h = dpf_aes::mmo_hash(s, lk, SelectRK{rkl.k, rkd.k, 0u - bit});
+  uint32_t m = 0u - t;
+  h.w0 ^= cs.x & m; h.w1 ^= cs.y & m; h.w2 ^= cs.z & m; h.w3 ^= cs.w & m;
+  uint32_t nt = h.w0 & 1u;
+  h.w0 &= ~1u;
+  nt ^= t & ((cctl >> bit) & 1u);
+  s = h;
+  t = nt;
+}
+
+// ------------------------------------------------------------------------
+// Leaf conversion + correction (a12/a13)
+// ------------------------------------------------------------------------
+
+// Element-wise add/neg of a 128-bit block viewed as 128/BITS little-endian lanes.
+template <int BITS>
+__device__ __forceinline__ Block4 lanes_add(Block4 a, Block4 b) {
+  if constexpr (BITS == 128) {
+    uint64_t alo = ((uint64_t)a.w1 << 32) | a.w0, ahi = ((uint64_t)a.w3 << 32) | a.w2;
+    uint64_t blo = ((uint64_t)b.w1 << 32) | b.w0, bhi = ((uint64_t)b.w3 << 32) | b.w2;
+    uint64_t lo = alo + blo, hi = ahi + bhi + (lo < alo ? 1 : 0);
+    return Block4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  } else if constexpr (BITS == 64) {
+    uint64_t lo = (((uint64_t)a.w1 << 32) | a.w0) + (((uint64_t)b.w1 << 32) | b.w0);
+    uint64_t hi = (((uint64_t)a.w3 << 32) | a.w2) + (((uint64_t)b.w3 << 32) | b.w2);
+    return Block4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  } else if constexpr (BITS == 32) {
+    return Block4{a.w0 + b.w0, a.w1 + b.w1, a.w2 + b.w2, a.w3 + b.w3};
+  } else {
+    constexpr uint32_t H = BITS == 16 ? 0x80008000u : 0x80808080u;
+    auto f = [](uint32_t x, uint32_t y) { return ((x & ~H) + (y & ~H)) ^ ((x ^ y) & H); };
+    return Block4{f(a.w0, b.w0), f(a.w1, b.w1), f(a.w2, b.w2), f(a.w3, b.w3)};
+  }
+}
+template <int BITS>
+__device__ __forceinline__ Block4 lanes_neg(Block4 a) {
+  if constexpr (BITS == 128) {
+    uint64_t lo = ((uint64_t)a.w1 << 32) | a.w0, hi = ((uint64_t)a.w3 << 32) | a.w2;
+    uint64_t nlo = 0 - lo, nhi = 0 - hi - (lo != 0 ? 1 : 0);
+    return Block4{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
+  } else if constexpr (BITS == 64) {
+    uint64_t lo = 0 - (((uint64_t)a.w1 << 32) | a.w0);
+    uint64_t hi = 0 - (((uint64_t)a.w3 << 32) | a.w2);
+    return Block4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  } else if constexpr (BITS == 32) {
+    return Block4{0u - a.w0, 0u - a.w1, 0u - a.w2, 0u - a.w3};
+  } else {
+    constexpr uint32_t H = BITS == 16 ? 0x80008000u : 0x80808080u;
+    auto f = [](uint32_t x) { return (H - (x & ~H)) ^ (~x & H); };
+    return Block4{f(a.w0), f(a.w1), f(a.w2), f(a.w3)};
+  }
+}
+
+// Plain unsigned integers and XorWrapper of them with b == 1: the hashed block
+// *is* the element array (value_type_helpers.h:199-211), the correction word is
+// one block in the same layout.
+template <int BITS, bool XOR>
+struct FastIntLeaf {
+  const dpf_block* vcw_elems;  // E elements, one dpf_block each (device)
+  int E;
+  int party;
+  int store_bytes;    // elements_per_leaf * BITS / 8 (1..16)
+  Block4 vcw;         // value correction packed as E lanes of BITS (set by init)
+
+  // Packs the per-element correction into one block (value_type_helpers.h:597-631
+  // produces E elements whose concatenation has the hashed block's layout).
+  __device__ __forceinline__ void init() {
+    unsigned __int128 packed = 0;
+    for (int e = E - 1; e >= 0; --e) {
+      dpf_block c = vcw_elems[e];
+      unsigned __int128 v = ((unsigned __int128)c.high << 64) | c.low;
+      if (BITS < 128) {
+        v &= (((unsigned __int128)1 << (BITS & 127)) - 1);
+        packed = (packed << (BITS & 127)) | v;
+      } else {
+        packed = v;
+      }
+    }
+    vcw = Block4{(uint32_t)packed, (uint32_t)(packed >> 32), (uint32_t)(packed >> 64),
+                 (uint32_t)(packed >> 96)};
+  }
+
+  __device__ __forceinline__ Block4 correct(Block4 h, uint32_t t) const {
+    if (XOR) {
+      uint32_t m = 0u - t;
+      return Block4{h.w0 ^ (vcw.w0 & m), h.w1 ^ (vcw.w1 & m), h.w2 ^ (vcw.w2 & m),
+                    h.w3 ^ (vcw.w3 & m)};
+    }
+    if (t) h = lanes_add<BITS>(h, vcw);
+    if (party == 1) h = lanes_neg<BITS>(h);
+    return h;
+  }
+
+  // Full-domain leaf: write elements_per_leaf elements.
+  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+                                       uint32_t t, int64_t leaf, char* out) const {
+    Block4 h = correct(dpf_aes::mmo_hash(seed, lk, UniformRK{rkv}), t);
+    char* p = out + leaf * (int64_t)store_bytes;
+    switch (store_bytes) {
+      case 16: *reinterpret_cast<uint4*>(p) = make_uint4(h.w0, h.w1, h.w2, h.w3); break;
+      case 8: *reinterpret_cast<uint2*>(p) = make_uint2(h.w0, h.w1); break;
+      case 4: *reinterpret_cast<uint32_t*>(p) = h.w0; break;
+      case 2: *reinterpret_cast<uint16_t*>(p) = (uint16_t)h.w0; break;
+      default: *reinterpret_cast<uint8_t*>(p) = (uint8_t)h.w0; break;
+    }
+  }
+};
+
+// Descriptor-driven conversion for Tuple / IntModN / multi-block types
+// (value_type_helpers.h:286-311, 415-443, 526-589).
+struct GenericLeaf {
+  dpf_value_desc d;
+  const dpf_block* vcw;   // E * num_leaves blocks
+  int party;
+  int elements_per_leaf;  // full domain: corrected elements per block
+  int esz;                // packed element size in bytes
+
+  __device__ __forceinline__ void init() {}
+
+  __device__ static unsigned __int128 load_le(const uint8_t* p, int n) {
+    unsigned __int128 v = 0;
+    for (int i = n - 1; i >= 0; --i) v = (v << 8) | p[i];
+    return v;
+  }
+  __device__ static unsigned __int128 mask(int bits) {
+    return bits >= 128 ? ~(unsigned __int128)0 : (((unsigned __int128)1 << bits) - 1);
+  }
+  __device__ unsigned __int128 modulus(int k) const {
+    return ((unsigned __int128)d.mod_high[k] << 64) | d.mod_low[k];
+  }
+  __device__ unsigned __int128 add(int k, unsigned __int128 a, unsigned __int128 b) const {
+    if (d.kind[k] == DPF_LEAF_XOR) return a ^ b;
+    if (d.kind[k] == DPF_LEAF_INTMODN) {
+      // IntModN += (int_mod_n.h:116-120, 208-223)
+      unsigned __int128 n = modulus(k), c = n - b;
+      return a >= c ? a - c : n - c + a;
+    }
+    return (a + b) & mask(d.bits[k]);
+  }
+  __device__ unsigned __int128 neg(int k, unsigned __int128 a) const {
+    if (d.kind[k] == DPF_LEAF_XOR) return a;
+    if (d.kind[k] == DPF_LEAF_INTMODN) return a == 0 ? 0 : modulus(k) - a;
+    return (0 - a) & mask(d.bits[k]);
+  }
+  __device__ static void store_le(char* p, unsigned __int128 v, int n) {
+    for (int i = 0; i < n; ++i) { p[i] = (char)(uint8_t)v; v >>= 8; }
+  }
+
+  // Hashes `seed` into b blocks and writes element `first .. first+count` of the
+  // converted array (after correction) to out_elem.
+  __device__ void convert_store(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+                                uint32_t t, int first, int count, char* out_elem) const {
+    uint8_t bytes[16 * kBMax];
+    const int b = d.blocks_needed;
+    for (int j = 0; j < b; ++j) {
+      Block4 h = dpf_aes::mmo_hash(add_small(seed, (uint32_t)j), lk, UniformRK{rkv});
+      uint32_t w[4] = {h.w0, h.w1, h.w2, h.w3};
+      for (int q = 0; q < 16; ++q) bytes[16 * j + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
+    }
+    const int nl = d.num_leaves;
+    if (d.direct) {
+      for (int e = first; e < first + count; ++e) {
+        int off = e * esz;
+        char* o = out_elem + (e - first) * esz;
+        for (int k = 0; k < nl; ++k) {
+          int lb = d.bits[k] >> 3;
+          unsigned __int128 v = load_le(bytes + off, lb);
+          if (t) {
+            dpf_block c = vcw[e * nl + k];
+            v = add(k, v, ((unsigned __int128)c.high << 64) | c.low);
+          }
+          if (party == 1) v = neg(k, v);
+          store_le(o, v, lb);
+          o += lb;
+          off += lb;
+        }
+      }
+      return;
+    }
+    // Sampling conversion: E == 1, every leaf but the last refills the block.
+    unsigned __int128 block = load_le(bytes, 16);
+    int rem = 16;
+    char* o = out_elem;
+    for (int k = 0; k < nl; ++k) {
+      int lb = d.bits[k] >> 3;
+      bool update = k + 1 < nl;
+      unsigned __int128 v;
+      if (d.kind[k] == DPF_LEAF_INTMODN) {
+        unsigned __int128 n = modulus(k);
+        unsigned __int128 q = block / n;
+        v = block - q * n;
+        if (update) {
+          block = lb < 16 ? (q << (8 * lb)) : 0;
+          block |= load_le(bytes + rem, lb);
+          rem += lb;
+        }
+      } else {
+        v = block & mask(d.bits[k]);
+        if (update) {
+          if (lb < 16) block &= ~mask(d.bits[k]); else block = 0;
+          block |= load_le(bytes + rem, lb);
+          rem += lb;
+        }
+      }
+      if (t) {
+        dpf_block c = vcw[k];
+        v = add(k, v, ((unsigned __int128)c.high << 64) | c.low);
+      }
+      if (party == 1) v = neg(k, v);
+      store_le(o, v, lb);
+      o += lb;
+    }
+  }
+
+  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+                                       uint32_t t, int64_t leaf, char* out) const {
+    convert_store(lk, rkv, seed, t, 0, elements_per_leaf,
+                  out + leaf * (int64_t)elements_per_leaf * esz);
+  }
+};
+
+// ------------------------------------------------------------------------
+// Kernels
+// ------------------------------------------------------------------------
+
+__global__ __launch_bounds__(kBlock) void hash_kernel(int64_t n, const dpf_block* __restrict__ in,
+                                                      dpf_block* __restrict__ out,
+                                                      RoundKeys rk) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  LdsLookup lk = make_lookup(lds);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    store_block(out + i, dpf_aes::mmo_hash(load_block(in + i), lk, UniformRK{rk.k}));
+  }
+}
+
+struct PathParams {
+  int64_t n;
+  int num_levels;
+  const dpf_block* seeds_in;
+  const uint8_t* ctrl_in;
+  const dpf_block* paths;
+  const dpf_block* cw_seed;
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  dpf_block* seeds_out;
+  uint8_t* ctrl_out;
+  RoundKeys rkl, rkd;
+};
+
+__device__ __forceinline__ uint32_t path_bit(Block4 p, int pos) {
+  uint32_t w = pos < 32 ? p.w0 : pos < 64 ? p.w1 : pos < 96 ? p.w2 : p.w3;
+  return (w >> (pos & 31)) & 1u;
+}
+
+__global__ __launch_bounds__(kBlock) void eval_paths_kernel(PathParams p) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  __syncthreads();
+  LdsLookup lk = make_lookup(lds);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p.n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    Block4 s = load_block(p.seeds_in + i);
+    uint32_t t = p.ctrl_in[i] & 1u;
+    Block4 path = load_block(p.paths + i);
+    for (int j = 0; j < p.num_levels; ++j) {
+      uint32_t bit = path_bit(path, p.num_levels - 1 - j);
+      path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
+    }
+    store_block(p.seeds_out + i, s);
+    p.ctrl_out[i] = (uint8_t)t;
+  }
+}
+
+struct ExpandParams {
+  int64_t num_items;  // num_starts << k0
+  int num_levels;     // L = k0 + S
+  int k0;             // levels walked per item (per-lane direction)
+  int S;              // subtree depth visited depth-first per item
+  const dpf_block* seeds_in;
+  const uint8_t* ctrl_in;
+  const dpf_block* cw_seed;
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  char* out;
+  RoundKeys rkl, rkr, rkv, rkd;
+};
+
+template <class Leaf>
+__global__ __launch_bounds__(kBlock) void expand_kernel(ExpandParams p, Leaf leaf) {
+  __shared__ LdsImage lds;
+  leaf.init();
+  fill_tables(lds.tab);
+  fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const int k0 = p.k0, S = p.S;
+  const int B = S >= 1 ? 1 : 0;  // leaf pairs share their parent
+  const int G = S - B;            // depth of the DFS stack
+  const int64_t ngroups = (int64_t)1 << G;
+  for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
+       item += (int64_t)gridDim.x * blockDim.x) {
+    // 1. walk from the start seed to this item's subtree root.
+    const int64_t r = item >> k0;
+    Block4 s = load_block(p.seeds_in + r);
+    uint32_t t = p.ctrl_in[r] & 1u;
+    for (int j = 0; j < k0; ++j) {
+      uint32_t bit = (uint32_t)((item >> (k0 - 1 - j)) & 1);
+      path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
+    }
+    // 2. depth-first over the subtree; stack[d] = node at depth d on the path.
+    Block4 st[kGMax + 1];
+    uint32_t tb = t;  // bit d = control bit of st[d]
+    st[0] = s;
+    const int64_t leaf_base = item << S;
+    for (int64_t g = 0; g < ngroups; ++g) {
+      int ds = 0;
+      uint32_t dir0 = 0;
+      if (g != 0) {
+        ds = G - 1 - (int)__builtin_ctzll((unsigned long long)g);
+        dir0 = 1;
+      }
+      Block4 node = st[0];
+      uint32_t nt = tb & 1u;
+#pragma unroll
+      for (int d = 0; d < kGMax; ++d) {
+        if (d >= ds && d < G) {  // wave-uniform
+          uint32_t dir = (d == ds) ? dir0 : 0u;
+          Block4 c;
+          uint32_t ct;
+          child_step(lk, dir ? p.rkr.k : p.rkl.k, st[d], (tb >> d) & 1u, dir,
+                     lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d], c, ct);
+          st[d + 1] = c;
+          tb = (tb & ~(1u << (d + 1))) | (ct << (d + 1));
+        }
+      }
+#pragma unroll
+      for (int d = 1; d <= kGMax; ++d)
+        if (d == G) { node = st[d]; nt = (tb >> d) & 1u; }
+      if (B == 0) {
+        leaf.emit(lk, p.rkv.k, node, nt, leaf_base + g, p.out);
+      } else {
+        const int lvl = k0 + G;
+        Block4 c0, c1;
+        uint32_t t0, t1;
+        child_step(lk, p.rkl.k, node, nt, 0u, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c0, t0);
+        child_step(lk, p.rkr.k, node, nt, 1u, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c1, t1);
+        leaf.emit(lk, p.rkv.k, c0, t0, leaf_base + 2 * g, p.out);
+        leaf.emit(lk, p.rkv.k, c1, t1, leaf_base + 2 * g + 1, p.out);
+      }
+    }
+  }
+}
+
+struct PointParams {
+  int64_t n;
+  int64_t points_per_key;
+  int num_levels;
+  const dpf_block* key_seed;
+  const uint8_t* party;
+  const dpf_block* seeds_in;
+  const uint8_t* ctrl_in;
+  const dpf_block* tree_index;
+  const int32_t* block_index;
+  const dpf_block* cw_seed;   // [key][level]
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  const dpf_block* vcw;       // [key][E * num_leaves]
+  int vcw_stride;             // E * num_leaves
+  char* out;
+  int esz;
+  RoundKeys rkl, rkd, rkv;
+};
+
+template <int BITS, bool XOR>
+__device__ __forceinline__ void point_store_fast(Block4 h, uint32_t t, int bi, dpf_block c,
+                                                 int party, char* o) {
+  // Element `bi` of the hashed block, corrected with its own correction value
+  // (distributed_point_function.h:993-1002).
+  unsigned __int128 x = ((unsigned __int128)h.w3 << 96) | ((unsigned __int128)h.w2 << 64) |
+                        ((unsigned __int128)h.w1 << 32) | h.w0;
+  unsigned __int128 cv = ((unsigned __int128)c.high << 64) | c.low;
+  if (BITS < 128) x >>= (bi * BITS) & 127;
+  if (XOR) {
+    if (t) x ^= cv;
+  } else {
+    if (t) x += cv;
+    if (party == 1) x = 0 - x;
+  }
+  if (BITS == 128) {
+    *reinterpret_cast<uint4*>(o) = make_uint4((uint32_t)x, (uint32_t)(x >> 32),
+                                              (uint32_t)(x >> 64), (uint32_t)(x >> 96));
+  } else if (BITS == 64) {
+    *reinterpret_cast<uint64_t*>(o) = (uint64_t)x;
+  } else if (BITS == 32) {
+    *reinterpret_cast<uint32_t*>(o) = (uint32_t)x;
+  } else if (BITS == 16) {
+    *reinterpret_cast<uint16_t*>(o) = (uint16_t)x;
+  } else {
+    *reinterpret_cast<uint8_t*>(o) = (uint8_t)x;
+  }
+}
+
+// Fused EvaluateAt for many keys: path walk + hash + convert + correct.
+template <class Leaf, int BITS, bool XOR, bool FAST>
+__global__ __launch_bounds__(kBlock) void eval_points_kernel(PointParams p, Leaf leaf) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const int L = p.num_levels;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p.n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = i / p.points_per_key;
+    int party = p.party[k] & 1;
+    Block4 s;
+    uint32_t t;
+    if (p.seeds_in) {
+      s = load_block(p.seeds_in + i);
+      t = p.ctrl_in[i] & 1u;
+    } else {
+      s = load_block(p.key_seed + k);
+      t = (uint32_t)party;
+    }
+    Block4 path = load_block(p.tree_index + i);
+    const dpf_block* cws = p.cw_seed + k * L;
+    const uint8_t* cl = p.cw_left + k * L;
+    const uint8_t* cr = p.cw_right + k * L;
+    for (int j = 0; j < L; ++j) {
+      uint32_t bit = path_bit(path, L - 1 - j);
+      Block4 c = load_block(cws + j);
+      uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
+      path_step(lk, p.rkl, p.rkd, s, t, bit, make_uint4(c.w0, c.w1, c.w2, c.w3), cctl);
+    }
+    int bi = p.block_index ? p.block_index[i] : 0;
+    char* o = p.out + i * (int64_t)p.esz;
+    if constexpr (FAST) {
+      Block4 h = dpf_aes::mmo_hash(s, lk, UniformRK{p.rkv.k});
+      point_store_fast<BITS, XOR>(h, t, bi, p.vcw[k * p.vcw_stride + bi], party, o);
+    } else {
+      Leaf lf = leaf;
+      lf.vcw = p.vcw + k * p.vcw_stride;
+      lf.party = party;
+      lf.convert_store(lk, p.rkv.k, s, t, bi, 1, o);
+    }
+  }
+}
+
+__global__ void gather_kernel(int64_t rows, int64_t count, int elem_size,
+                              const int64_t* __restrict__ src, const char* __restrict__ in,
+                              char* __restrict__ out) {
+  const int64_t total = rows * count * elem_size;
+  const int64_t row_bytes = count * elem_size;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i / row_bytes, c = i - r * row_bytes;
+    out[i] = in[src[r] * elem_size + c];
+  }
+}
+
+__global__ void sum_shares_kernel(int64_t num_keys, int64_t row_len, int bits, int xor_mode,
+                                  const char* __restrict__ shares, uint64_t* __restrict__ sums) {
+  const int eb = bits / 8;
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < row_len;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t acc = 0;
+    for (int64_t k = 0; k < num_keys; ++k) {
+      const char* p = shares + (k * row_len + j) * eb;
+      uint64_t v = 0;
+      if (eb == 8) v = *reinterpret_cast<const uint64_t*>(p);
+      else if (eb == 4) v = *reinterpret_cast<const uint32_t*>(p);
+      else if (eb == 2) v = *reinterpret_cast<const uint16_t*>(p);
+      else v = *reinterpret_cast<const uint8_t*>(p);
+      acc = xor_mode ? (acc ^ v) : (acc + v);
+    }
+    sums[j] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Host-side launch helpers
+// ------------------------------------------------------------------------
+int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+int grid_for(int64_t work_items) {
+  int64_t g = (work_items + kBlock - 1) / kBlock;
+  int64_t cap = num_cus();  // one 128 KiB-LDS workgroup per CU
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+int validate_desc(const dpf_value_desc* d) {
+  if (!d) return fail(kInvalidArgument, "value descriptor is NULL");
+  if (d->num_leaves < 1 || d->num_leaves > DPF_MAX_LEAVES)
+    return fail(kUnimplemented, "value type has too many leaves for the GPU path");
+  if (d->blocks_needed < 1 || d->blocks_needed > kBMax)
+    return fail(kUnimplemented, "value type needs too many AES blocks for the GPU path");
+  if (d->elements_per_block < 1) return fail(kInvalidArgument, "elements_per_block < 1");
+  for (int k = 0; k < d->num_leaves; ++k) {
+    int b = d->bits[k];
+    if (b < 8 || b > 128 || (b & (b - 1)))
+      return fail(kUnimplemented, "leaf bit size must be a power of two in [8, 128]");
+    if (d->kind[k] == DPF_LEAF_INTMODN && d->mod_low[k] == 0 && d->mod_high[k] == 0)
+      return fail(kInvalidArgument, "IntModN modulus is zero");
+  }
+  return kOk;
+}
+
+int packed_size(const dpf_value_desc* d) {
+  int s = 0;
+  for (int k = 0; k < d->num_leaves; ++k) s += d->bits[k] / 8;
+  return s;
+}
+
+bool fast_int(const dpf_value_desc* d) {
+  return d->num_leaves == 1 && d->direct && d->blocks_needed == 1 &&
+         d->kind[0] != DPF_LEAF_INTMODN;
+}
+
+RoundKeys xor_keys(const RoundKeys& a, const RoundKeys& b) {
+  RoundKeys r;
+  for (int i = 0; i < 44; ++i) r.k[i] = a.k[i] ^ b.k[i];
+  return r;
+}
+
+template <class Leaf>
+int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
+  hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid_for(p.num_items)), dim3(kBlock), 0, s, p,
+                     leaf);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+template <int BITS>
+int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf_block* vcw,
+                       int E, int party, int store_bytes, hipStream_t s) {
+  if (d->kind[0] == DPF_LEAF_XOR)
+    return launch_expand(p, FastIntLeaf<BITS, true>{vcw, E, party, store_bytes, {}}, s);
+  return launch_expand(p, FastIntLeaf<BITS, false>{vcw, E, party, store_bytes, {}}, s);
+}
+
+template <int BITS, bool XOR>
+int launch_points_fast(const PointParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((eval_points_kernel<GenericLeaf, BITS, XOR, true>),
+                     dim3(grid_for(p.n)), dim3(kBlock), 0, s, p, GenericLeaf{});
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+}  // namespace
+
+// ==========================================================================
+// C ABI
+// ==========================================================================
+extern "C" {
+
+int dpf_hip_abi_version(void) { return DPF_HIP_ABI_VERSION; }
+const char* dpf_hip_last_error(void) { return g_last_error.c_str(); }
+
+int dpf_hip_device_count(int* count) {
+  HIP_TRY(hipGetDeviceCount(count));
+  return kOk;
+}
+int dpf_hip_set_device(int device) {
+  HIP_TRY(hipSetDevice(device));
+  return kOk;
+}
+int dpf_hip_alloc(void** ptr, size_t bytes) {
+  if (!ptr) return fail(kInvalidArgument, "ptr is NULL");
+  *ptr = nullptr;
+  if (bytes == 0) bytes = 1;
+  HIP_TRY(hipMalloc(ptr, bytes));
+  return kOk;
+}
+int dpf_hip_free(void* ptr) {
+  if (ptr) HIP_TRY(hipFree(ptr));
+  return kOk;
+}
+int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return kOk;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return kOk;
+}
+int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return kOk;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return kOk;
+}
+int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return kOk;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return kOk;
+}
+int dpf_hip_memset(void* dst, int value, size_t bytes, void* stream) {
+  if (!bytes) return kOk;
+  HIP_TRY(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));
+  return kOk;
+}
+int dpf_hip_stream_sync(void* stream) {
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return kOk;
+}
+int dpf_hip_packed_element_size(const dpf_value_desc* desc) {
+  if (!desc) return -1;
+  return packed_size(desc);
+}
+
+int dpf_hip_hash(int64_t n, const dpf_block* in, const dpf_aes_key* key, dpf_block* out,
+                 void* stream) {
+  if (n < 0) return fail(kInvalidArgument, "n < 0");
+  if (n == 0) return kOk;
+  if (!in || !out || !key) return fail(kInvalidArgument, "NULL pointer");
+  hipLaunchKernelGGL(hash_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n,
+                     in, out, expand_key(key));
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_eval_paths(int64_t num_seeds, int num_levels, const dpf_block* seeds_in,
+                       const uint8_t* control_in, const dpf_block* paths,
+                       const dpf_block* cw_seed, const uint8_t* cw_left, const uint8_t* cw_right,
+                       const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                       dpf_block* seeds_out, uint8_t* control_out, void* stream) {
+  if (num_seeds < 0 || num_levels < 0 || num_levels > kMaxCwLevels)
+    return fail(kInvalidArgument, "num_seeds or num_levels out of range");
+  if (num_seeds == 0) return kOk;
+  hipStream_t s = (hipStream_t)stream;
+  if (num_levels == 0) {
+    if (seeds_out != seeds_in)
+      HIP_TRY(hipMemcpyAsync(seeds_out, seeds_in, num_seeds * sizeof(dpf_block),
+                             hipMemcpyDeviceToDevice, s));
+    if (control_out != control_in)
+      HIP_TRY(hipMemcpyAsync(control_out, control_in, num_seeds, hipMemcpyDeviceToDevice, s));
+    return kOk;
+  }
+  if (!seeds_in || !control_in || !paths || !cw_seed || !cw_left || !cw_right || !key_left ||
+      !key_right || !seeds_out || !control_out)
+    return fail(kInvalidArgument, "NULL pointer");
+  PathParams p;
+  p.n = num_seeds;
+  p.num_levels = num_levels;
+  p.seeds_in = seeds_in;
+  p.ctrl_in = control_in;
+  p.paths = paths;
+  p.cw_seed = cw_seed;
+  p.cw_left = cw_left;
+  p.cw_right = cw_right;
+  p.seeds_out = seeds_out;
+  p.ctrl_out = control_out;
+  p.rkl = expand_key(key_left);
+  p.rkd = xor_keys(p.rkl, expand_key(key_right));
+  hipLaunchKernelGGL(eval_paths_kernel, dim3(grid_for(num_seeds)), dim3(kBlock), 0, s, p);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t* control_in,
+                   int num_levels, const dpf_block* cw_seed, const uint8_t* cw_left,
+                   const uint8_t* cw_right, const dpf_aes_key* key_left,
+                   const dpf_aes_key* key_right, const dpf_aes_key* key_value,
+                   const dpf_value_desc* desc, int elements_per_leaf,
+                   const dpf_block* value_correction, int party, void* out, void* stream) {
+  int st = validate_desc(desc);
+  if (st) return st;
+  if (num_starts < 0 || num_levels < 0 || num_levels > 62)
+    return fail(kInvalidArgument, "num_starts or num_levels out of range");
+  if (elements_per_leaf < 1 || elements_per_leaf > desc->elements_per_block)
+    return fail(kInvalidArgument, "elements_per_leaf must be in [1, elements_per_block]");
+  if (num_starts == 0) return kOk;
+  if (!seeds_in || !control_in || !key_left || !key_right || !key_value || !value_correction ||
+      !out || (num_levels > 0 && (!cw_seed || !cw_left || !cw_right)))
+    return fail(kInvalidArgument, "NULL pointer");
+  if (num_starts > (INT64_MAX >> num_levels))
+    return fail(kInvalidArgument, "expansion too large");
+  // Choose the depth-first subtree depth S and the per-item walk depth k0.
+  const int64_t threads = (int64_t)num_cus() * kBlock;
+  int S = num_levels < kSMax ? num_levels : kSMax;
+  const int s_min = num_levels < 4 ? num_levels : 4;
+  while (S > s_min && (num_starts << (num_levels - S)) < threads) --S;
+  ExpandParams p;
+  p.num_levels = num_levels;
+  p.S = S;
+  p.k0 = num_levels - S;
+  p.num_items = num_starts << p.k0;
+  p.seeds_in = seeds_in;
+  p.ctrl_in = control_in;
+  p.cw_seed = cw_seed;
+  p.cw_left = cw_left;
+  p.cw_right = cw_right;
+  p.out = (char*)out;
+  p.rkl = expand_key(key_left);
+  p.rkr = expand_key(key_right);
+  p.rkv = expand_key(key_value);
+  p.rkd = xor_keys(p.rkl, p.rkr);
+  hipStream_t s = (hipStream_t)stream;
+  if (fast_int(desc)) {
+    const int bits = desc->bits[0], E = desc->elements_per_block;
+    const int store_bytes = elements_per_leaf * bits / 8;
+    switch (bits) {
+      case 8: return launch_expand_fast<8>(p, desc, value_correction, E, party, store_bytes, s);
+      case 16: return launch_expand_fast<16>(p, desc, value_correction, E, party, store_bytes, s);
+      case 32: return launch_expand_fast<32>(p, desc, value_correction, E, party, store_bytes, s);
+      case 64: return launch_expand_fast<64>(p, desc, value_correction, E, party, store_bytes, s);
+      default: return launch_expand_fast<128>(p, desc, value_correction, E, party, store_bytes, s);
+    }
+  }
+  GenericLeaf g;
+  g.d = *desc;
+  g.vcw = value_correction;
+  g.party = party;
+  g.elements_per_leaf = elements_per_leaf;
+  g.esz = packed_size(desc);
+  return launch_expand(p, g, s);
+}
+
+int dpf_hip_eval_points(int64_t num_points, int64_t points_per_key, int num_levels,
+                        const dpf_block* key_seed, const uint8_t* party,
+                        const dpf_block* seeds_in, const uint8_t* control_in,
+                        const dpf_block* tree_index, const int32_t* block_index,
+                        const dpf_block* cw_seed, const uint8_t* cw_left, const uint8_t* cw_right,
+                        const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                        const dpf_aes_key* key_value, const dpf_value_desc* desc,
+                        const dpf_block* value_correction, void* out, void* stream) {
+  int st = validate_desc(desc);
+  if (st) return st;
+  if (num_points < 0 || points_per_key < 1 || num_levels < 0 || num_levels > 128)
+    return fail(kInvalidArgument, "num_points, points_per_key or num_levels out of range");
+  if (num_points == 0) return kOk;
+  if (!party || !tree_index || !key_left || !key_right || !key_value || !value_correction ||
+      !out || (!seeds_in && !key_seed) || (seeds_in && !control_in) ||
+      (num_levels > 0 && (!cw_seed || !cw_left || !cw_right)))
+    return fail(kInvalidArgument, "NULL pointer");
+  PointParams p;
+  p.n = num_points;
+  p.points_per_key = points_per_key;
+  p.num_levels = num_levels;
+  p.key_seed = key_seed;
+  p.party = party;
+  p.seeds_in = seeds_in;
+  p.ctrl_in = control_in;
+  p.tree_index = tree_index;
+  p.block_index = block_index;
+  p.cw_seed = cw_seed;
+  p.cw_left = cw_left;
+  p.cw_right = cw_right;
+  p.vcw = value_correction;
+  p.vcw_stride = desc->elements_per_block * desc->num_leaves;
+  p.out = (char*)out;
+  p.esz = packed_size(desc);
+  p.rkl = expand_key(key_left);
+  p.rkd = xor_keys(p.rkl, expand_key(key_right));
+  p.rkv = expand_key(key_value);
+  hipStream_t s = (hipStream_t)stream;
+  if (fast_int(desc)) {
+    const bool x = desc->kind[0] == DPF_LEAF_XOR;
+    switch (desc->bits[0]) {
+      case 8: return x ? launch_points_fast<8, true>(p, s) : launch_points_fast<8, false>(p, s);
+      case 16: return x ? launch_points_fast<16, true>(p, s) : launch_points_fast<16, false>(p, s);
+      case 32: return x ? launch_points_fast<32, true>(p, s) : launch_points_fast<32, false>(p, s);
+      case 64: return x ? launch_points_fast<64, true>(p, s) : launch_points_fast<64, false>(p, s);
+      default: return x ? launch_points_fast<128, true>(p, s) : launch_points_fast<128, false>(p, s);
+    }
+  }
+  GenericLeaf g;
+  g.d = *desc;
+  g.vcw = value_correction;
+  g.party = 0;
+  g.elements_per_leaf = 1;
+  g.esz = p.esz;
+  hipLaunchKernelGGL((eval_points_kernel<GenericLeaf, 8, false, false>), dim3(grid_for(num_points)),
+                     dim3(kBlock), 0, s, p, g);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_gather(int64_t num_rows, int64_t count, int elem_size, const int64_t* src_offset,
+                   const void* in, void* out, void* stream) {
+  if (num_rows < 0 || count < 0 || elem_size < 1) return fail(kInvalidArgument, "bad sizes");
+  int64_t total = num_rows * count * elem_size;
+  if (total == 0) return kOk;
+  int64_t g = (total + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+                     num_rows, count, elem_size, src_offset, (const char*)in, (char*)out);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_sum_shares_u64(int64_t num_keys, int64_t row_len, int bits, int xor_mode,
+                           const void* shares, uint64_t* sums, void* stream) {
+  if (num_keys < 0 || row_len < 0 || !(bits == 8 || bits == 16 || bits == 32 || bits == 64))
+    return fail(kInvalidArgument, "bad arguments");
+  if (row_len == 0) return kOk;
+  int64_t g = (row_len + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(sum_shares_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+                     num_keys, row_len, bits, xor_mode, (const char*)shares, sums);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_event_create(void** ev) {
+  HIP_TRY(hipEventCreate((hipEvent_t*)ev));
+  return kOk;
+}
+int dpf_hip_event_destroy(void* ev) {
+  HIP_TRY(hipEventDestroy((hipEvent_t)ev));
+  return kOk;
+}
+int dpf_hip_event_record(void* ev, void* stream) {
+  HIP_TRY(hipEventRecord((hipEvent_t)ev, (hipStream_t)stream));
+  return kOk;
+}
+int dpf_hip_event_elapsed_ms(void* start, void* stop, float* ms) {
+  HIP_TRY(hipEventSynchronize((hipEvent_t)stop));
+  HIP_TRY(hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop));
+  return kOk;
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+/*
+ * dpf_hip.h -- C ABI of the MI355X (gfx950) DPF evaluation engine.
+ *
+ * This is the drop-in seam between a host DistributedPointFunction and the
+ * HIP kernels.  It replaces the reference's CPU hot loops:
+ *
+ *   dpf_hip_hash        <- Aes128FixedKeyHash::Evaluate
+ *                          (dpf/aes_128_fixed_key_hash.h:51-52, .cc:47-85)
+ *   dpf_hip_eval_paths  <- dpf_internal::EvaluateSeeds
+ *                          (dpf/internal/evaluate_prg_hwy.h:58-64, .cc:495-506)
+ *   dpf_hip_expand      <- DistributedPointFunction::ExpandSeeds + HashExpandedSeeds
+ *                          + the EvaluateUntil value-correction loop, fused
+ *                          (dpf/distributed_point_function.cc:271-349, 500-524;
+ *                           dpf/distributed_point_function.h:785-808)
+ *   dpf_hip_eval_points <- EvaluateAtImpl's EvaluateSeeds + HashExpandedSeeds +
+ *                          per-point correction, fused, for one or many keys
+ *                          (dpf/distributed_point_function.h:839-1010)
+ *
+ * Conventions
+ *   - Every function returns an int status: 0 = OK, otherwise the absl status
+ *     code number (3 INVALID_ARGUMENT, 8 RESOURCE_EXHAUSTED, 12 UNIMPLEMENTED,
+ *     13 INTERNAL).  dpf_hip_last_error() returns a message for the last failure
+ *     on the calling thread.
+ *   - All array pointers passed to compute entry points are DEVICE pointers,
+ *     caller-owned.  Allocation only crosses the ABI through dpf_hip_alloc /
+ *     dpf_hip_free; copies through dpf_hip_memcpy_*.
+ *   - A 128-bit block (dpf_block) is the absl::uint128 memory image:
+ *     {low, high}, little-endian.  Booleans are one byte (0/1).
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).  Compute
+ *     entry points are asynchronous on that stream (no host synchronisation);
+ *     dpf_hip_stream_sync() waits.
+ *   - Not thread-safe per stream (the reference is single-threaded too,
+ *     dpf/aes_128_fixed_key_hash.h:77).
+ */
+#ifndef DPF_HIP_H_
+#define DPF_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPF_HIP_ABI_VERSION 1
+#define DPF_MAX_LEAVES 16
+
+typedef struct dpf_block {
+  uint64_t low;
+  uint64_t high;
+} dpf_block;
+
+/* One fixed AES-128 key: the 16-byte memory image of the uint128 key
+ * (aes_128_fixed_key_hash.cc:38-40). */
+typedef struct dpf_aes_key {
+  uint8_t bytes[16];
+} dpf_aes_key;
+
+/* Leaf kinds of a flattened ValueType (distributed_point_function.proto:25-60). */
+enum dpf_leaf_kind { DPF_LEAF_INT = 0, DPF_LEAF_INTMODN = 1, DPF_LEAF_XOR = 2 };
+
+/* A ValueType flattened into its integer leaves in declaration order, plus the
+ * per-hierarchy-level sampling parameters the host computed:
+ *   direct            CanBeConvertedDirectly (value_type_helpers.h:342-344)
+ *   elements_per_block ElementsPerBlock<T>() (value_type_helpers.h:508-520)
+ *   blocks_needed     ceil(BitsNeeded / 128) (distributed_point_function.cc:578-587) */
+typedef struct dpf_value_desc {
+  int32_t num_leaves;
+  int32_t direct;
+  int32_t elements_per_block;
+  int32_t blocks_needed;
+  int32_t kind[DPF_MAX_LEAVES];
+  int32_t bits[DPF_MAX_LEAVES];
+  uint64_t mod_low[DPF_MAX_LEAVES];
+  uint64_t mod_high[DPF_MAX_LEAVES];
+} dpf_value_desc;
+
+/* ---- runtime / memory ---------------------------------------------------- */
+int dpf_hip_abi_version(void);
+const char* dpf_hip_last_error(void);
+int dpf_hip_device_count(int* count);
+int dpf_hip_set_device(int device);
+int dpf_hip_alloc(void** ptr, size_t bytes);
+int dpf_hip_free(void* ptr);
+int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
+int dpf_hip_memset(void* dst, int value, size_t bytes, void* stream);
+int dpf_hip_stream_sync(void* stream);
+/* Packed size in bytes of one output element: sum of leaf bits / 8. */
+int dpf_hip_packed_element_size(const dpf_value_desc* desc);
+
+/* ---- a1: out[i] = AES_key(sigma(in[i])) ^ sigma(in[i]) --------------------
+ * Replaces Aes128FixedKeyHash::Evaluate (aes_128_fixed_key_hash.cc:47-85).
+ * in/out may alias. */
+int dpf_hip_hash(int64_t n, const dpf_block* in, const dpf_aes_key* key,
+                 dpf_block* out, void* stream);
+
+/* ---- a9: path evaluation --------------------------------------------------
+ * Replaces dpf_internal::EvaluateSeeds (evaluate_prg_hwy.h:58-64).  For each
+ * seed i and level j < num_levels: bit = (paths[i] >> (num_levels-1-j)) & 1,
+ * s = H_{bit ? right : left}(s); if t: s ^= cw_seed[j]; t' = s & 1; s &= ~1;
+ * if t: t' ^= bit ? cw_right[j] : cw_left[j].  Outputs may alias inputs.
+ * With num_levels == 0 the inputs are copied to the outputs. */
+int dpf_hip_eval_paths(int64_t num_seeds, int num_levels, const dpf_block* seeds_in,
+                       const uint8_t* control_in, const dpf_block* paths,
+                       const dpf_block* cw_seed, const uint8_t* cw_left,
+                       const uint8_t* cw_right, const dpf_aes_key* key_left,
+                       const dpf_aes_key* key_right, dpf_block* seeds_out,
+                       uint8_t* control_out, void* stream);
+
+/* ---- a4+a5+a6+a12+a13: fused subtree expansion + leaf hashing/correction ---
+ * Replaces ExpandSeeds (cc:271-349) + HashExpandedSeeds (cc:500-524) + the
+ * EvaluateUntil correction loop (h:785-808).  Expands each of num_starts
+ * (seed, control) pairs through num_levels levels (child 2j = left, 2j+1 =
+ * right), hashes every leaf seed with key_value into desc->blocks_needed blocks
+ * (seed + j), converts them to desc->elements_per_block elements, keeps the
+ * first `elements_per_leaf` (= corrected_elements_per_block), adds
+ * value_correction (elements_per_block * num_leaves dpf_blocks, one per leaf
+ * value) when the leaf's control bit is set and negates when party == 1.
+ * Writes (num_starts << num_levels) * elements_per_leaf packed elements to
+ * `out` in expansion order. */
+int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t* control_in,
+                   int num_levels, const dpf_block* cw_seed, const uint8_t* cw_left,
+                   const uint8_t* cw_right, const dpf_aes_key* key_left,
+                   const dpf_aes_key* key_right, const dpf_aes_key* key_value,
+                   const dpf_value_desc* desc, int elements_per_leaf,
+                   const dpf_block* value_correction, int party, void* out, void* stream);
+
+/* ---- a11: fused point evaluation for many keys ----------------------------
+ * Replaces EvaluateAtImpl's path walk + hash + correction (h:930-1003).
+ * Point i belongs to key k = i / points_per_key.  Its walk starts at
+ * (seeds_in[i], control_in[i]) if seeds_in != NULL, else at the key's root
+ * (key_seed[k], party[k]).  The path is tree_index[i] over num_levels levels
+ * using key k's correction words cw_seed[k*num_levels + j], cw_left[...],
+ * cw_right[...].  The element block_index[i] (NULL = 0) of the hashed leaf is
+ * corrected with value_correction[k * E*num_leaves ...] and negated if
+ * party[k] == 1, then written packed to out[i]. */
+int dpf_hip_eval_points(int64_t num_points, int64_t points_per_key, int num_levels,
+                        const dpf_block* key_seed, const uint8_t* party,
+                        const dpf_block* seeds_in, const uint8_t* control_in,
+                        const dpf_block* tree_index, const int32_t* block_index,
+                        const dpf_block* cw_seed, const uint8_t* cw_left,
+                        const uint8_t* cw_right, const dpf_aes_key* key_left,
+                        const dpf_aes_key* key_right, const dpf_aes_key* key_value,
+                        const dpf_value_desc* desc, const dpf_block* value_correction,
+                        void* out, void* stream);
+
+/* ---- gather for EvaluateUntil with prefixes (h:822-835) -------------------
+ * out[i*count + j] = in[src_offset[i] + j], elements of elem_size bytes. */
+int dpf_hip_gather(int64_t num_rows, int64_t count, int elem_size, const int64_t* src_offset,
+                   const void* in, void* out, void* stream);
+
+/* ---- multi-key share aggregation ------------------------------
+ * sums[j] = sum over k < num_keys of shares[k*row_len + j] for plain integer
+ * leaves of `bits` (8..64) widened to uint64 (mod 2^64), or XOR for xor != 0. */
+int dpf_hip_sum_shares_u64(int64_t num_keys, int64_t row_len, int bits, int xor_mode,
+                           const void* shares, uint64_t* sums, void* stream);
+
+/* ---- timing helpers (hipEvents on the given stream) ------------------------ */
+int dpf_hip_event_create(void** ev);
+int dpf_hip_event_destroy(void* ev);
+int dpf_hip_event_record(void* ev, void* stream);
+int dpf_hip_event_elapsed_ms(void* start, void* stop, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DPF_HIP_H_ */

@@ -1,0 +1,222 @@
+"""Parity of the gfx950 kernels (through the C ABI) against the CPU oracle.
+
+Every comparison is bit-exact.  Inputs are seeded; sizes are small enough for
+the oracle to finish in seconds.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+KEY0 = 0
+KEY1 = O.make_uint128(0x1111111111111111, 0x1111111111111111)
+SEED0 = O.make_uint128(0x0123012301230123, 0x0123012301230123)
+SEED1 = O.make_uint128(0x4567456745674567, 0x4567456745674567)
+
+
+@pytest.fixture(scope="module")
+def hip():
+    import torch
+    from distributed_point_functions_amd import hip_abi
+    hip_abi.load(require_gpu=True)
+    assert torch.cuda.is_available()
+    return hip_abi
+
+
+def _rand_blocks(rng, n):
+    return rng.integers(0, 2**64, size=(n, 2), dtype=np.uint64)
+
+
+def test_hash_known_answer(hip):
+    # dpf/aes_128_fixed_key_hash_test.cc:114-135
+    x = hip.to_device_blocks(O.blocks_from_ints([SEED0, SEED1]))
+    out0 = O.ints_from_blocks(hip.blocks_to_numpy(hip.hash_blocks(x, KEY0)))
+    out1 = O.ints_from_blocks(hip.blocks_to_numpy(hip.hash_blocks(x, KEY1)))
+    assert out0 == [O.make_uint128(0x73C2DC14812BE4EF, 0xEAC64D09C8ADF8ED),
+                    O.make_uint128(0xB8F33653A53A8436, 0xAEDF39B62DE91D95)]
+    assert out1 == [O.make_uint128(0x934704AFF58FA233, 0xD3C20D1B9CC18D8F),
+                    O.make_uint128(0x530098817046D284, 0x43E61D3273A04F7C)]
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 1000, 300_001])
+@pytest.mark.parametrize("key", [O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE])
+def test_hash_random(hip, n, key):
+    rng = np.random.default_rng(n)
+    x = _rand_blocks(rng, n)
+    got = hip.blocks_to_numpy(hip.hash_blocks(hip.to_device_blocks(x), key))
+    np.testing.assert_array_equal(got, O.aes_hash(key, x))
+
+
+def test_hash_in_place(hip):
+    rng = np.random.default_rng(7)
+    x = _rand_blocks(rng, 4097)
+    d = hip.to_device_blocks(x)
+    hip.hash_blocks(d, O.PRG_KEY_VALUE, out=d)
+    np.testing.assert_array_equal(hip.blocks_to_numpy(d), O.aes_hash(O.PRG_KEY_VALUE, x))
+
+
+def _hwy_test_inputs(num_seeds, num_levels):
+    """Deterministic inputs of dpf/internal/evaluate_prg_hwy_test.cc:55-86."""
+    seeds = O.blocks_from_ints([O.make_uint128(i, i + 1) for i in range(num_seeds)])
+    paths = O.blocks_from_ints([O.make_uint128(23 * i + 42, 42 * i + 23) for i in range(num_seeds)])
+    ctrl = np.array([1 if i % 7 == 0 else 0 for i in range(num_seeds)], np.uint8)
+    cws = O.blocks_from_ints([O.make_uint128(i + 1, i) for i in range(num_levels)])
+    cl = np.array([1 if i % 23 == 0 else 0 for i in range(num_levels)], np.uint8)
+    cr = np.array([1 if i % 42 != 0 else 0 for i in range(num_levels)], np.uint8)
+    return seeds, ctrl, paths, cws, cl, cr
+
+
+@pytest.mark.parametrize("num_seeds", [1, 2, 101, 128, 1000])
+@pytest.mark.parametrize("num_levels", [0, 1, 2, 32, 63, 64, 127])
+def test_eval_paths_matches_reference_grid(hip, num_seeds, num_levels):
+    seeds, ctrl, paths, cws, cl, cr = _hwy_test_inputs(num_seeds, num_levels)
+    want_s, want_c = O.evaluate_seeds(seeds, ctrl, paths, cws, cl, cr, KEY0, KEY1)
+    d = [hip.to_device_blocks(seeds), hip.to_device_u8(ctrl), hip.to_device_blocks(paths),
+         hip.to_device_blocks(cws if len(cws) else np.zeros((1, 2), np.uint64)),
+         hip.to_device_u8(cl if len(cl) else np.zeros(1, np.uint8)),
+         hip.to_device_u8(cr if len(cr) else np.zeros(1, np.uint8))]
+    import torch
+    cl_t = d[4][:num_levels]
+    cr_t = d[5][:num_levels]
+    s, c = hip.eval_paths(d[0], d[1], d[2], d[3], cl_t, cr_t, KEY0, KEY1)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(hip.blocks_to_numpy(s), want_s)
+    np.testing.assert_array_equal(c.cpu().numpy(), want_c)
+
+
+def _desc(hip, vt, b):
+    return hip.value_desc(O.leaves(vt), O.is_direct(vt), O.elements_per_block(vt), b)
+
+
+def _rand_value(rng, vt):
+    out = []
+    for kind, bits, mod in O.leaves(vt):
+        if kind == O.LEAF_INTMODN:
+            out.append(int(rng.integers(0, 2**62)) % mod)
+        else:
+            out.append(int.from_bytes(rng.bytes(bits // 8), "little"))
+    return out
+
+
+FAST_TYPES = [("int", 8), ("int", 16), ("int", 32), ("int", 64), ("int", 128),
+              ("xor", 8), ("xor", 32), ("xor", 64), ("xor", 128)]
+M32 = 4294967291
+M64 = 18446744073709551557
+M80 = O.make_uint128(65535, 18446744073709551551)
+GENERIC_TYPES = [
+    ("tuple", [("int", 32), ("int", 64)]),
+    ("tuple", [("int", 8), ("int", 16), ("int", 32), ("int", 64)]),
+    ("tuple", [("int", 32), ("tuple", [("int", 32), ("int", 32)]), ("int", 32)]),
+    ("tuple", [("int", 32), ("int", 128)]),
+    ("tuple", [("int", 32), ("int", 32)]),
+    ("tuple", [("int", 8)]),
+    ("intmodn", 32, M32),
+    ("tuple", [("intmodn", 32, M32), ("intmodn", 32, M32)]),
+    ("tuple", [("int", 32), ("intmodn", 32, M32)]),
+    ("tuple", [("int", 128), ("intmodn", 32, M32)]),
+    ("tuple", [("intmodn", 64, M64)] * 5),
+    ("tuple", [("intmodn", 128, M80), ("intmodn", 128, M80)]),
+    ("tuple", [("xor", 32), ("int", 128)]),
+]
+
+
+def _expand_case(hip, rng, vt, n0, levels, party, sec=48.0, cepb=None):
+    b = (O.bits_needed(vt, sec) + 127) // 128
+    E = O.elements_per_block(vt)
+    cepb = cepb or E
+    seeds = _rand_blocks(rng, n0)
+    ctrl = rng.integers(0, 2, size=n0, dtype=np.uint8)
+    cws = _rand_blocks(rng, max(levels, 1))
+    cl = rng.integers(0, 2, size=max(levels, 1), dtype=np.uint8)
+    cr = rng.integers(0, 2, size=max(levels, 1), dtype=np.uint8)
+    vcw = [_rand_value(rng, vt) for _ in range(E)]
+    es, ec = O.expand_seeds(seeds, ctrl, cws[:levels], cl[:levels], cr[:levels])
+    want = O.hash_correct(vt, es, ec, b, cepb, vcw, party)
+    import torch
+    got = hip.expand(hip.to_device_blocks(seeds), hip.to_device_u8(ctrl),
+                     hip.to_device_blocks(cws), hip.to_device_u8(cl)[:levels],
+                     hip.to_device_u8(cr)[:levels],
+                     (O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE), _desc(hip, vt, b), cepb,
+                     hip.to_device_blocks(O._leaf_array(vcw)), party)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().reshape(want.shape), want)
+
+
+@pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
+@pytest.mark.parametrize("levels,n0", [(0, 1), (1, 1), (3, 2), (9, 1), (14, 1), (6, 37)])
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_fast_types(hip, vt, levels, n0, party):
+    rng = np.random.default_rng(hash((str(vt), levels, n0, party)) & 0xFFFFFFFF)
+    _expand_case(hip, rng, vt, n0, levels, party)
+
+
+@pytest.mark.parametrize("vt,cepb", [(("int", 8), 1), (("int", 8), 4), (("int", 16), 2),
+                                     (("int", 32), 1), (("int", 64), 1)], ids=str)
+def test_expand_partial_blocks(hip, vt, cepb):
+    # Small domains: fewer corrected elements than ElementsPerBlock (h:785-791).
+    _expand_case(hip, np.random.default_rng(cepb), vt, 1, 5, 1, cepb=cepb)
+
+
+@pytest.mark.parametrize("vt", GENERIC_TYPES, ids=str)
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_generic_types(hip, vt, party):
+    rng = np.random.default_rng(len(str(vt)) * 7 + party)
+    _expand_case(hip, rng, vt, 2, 7, party)
+
+
+def _points_case(hip, rng, vt, num_keys, ppk, levels, sec=48.0, from_partials=False):
+    b = (O.bits_needed(vt, sec) + 127) // 128
+    E = O.elements_per_block(vt)
+    n = num_keys * ppk
+    key_seed = _rand_blocks(rng, num_keys)
+    party = rng.integers(0, 2, size=num_keys, dtype=np.uint8)
+    cws = _rand_blocks(rng, max(num_keys * levels, 1))
+    cl = rng.integers(0, 2, size=max(num_keys * levels, 1), dtype=np.uint8)
+    cr = rng.integers(0, 2, size=max(num_keys * levels, 1), dtype=np.uint8)
+    tree = _rand_blocks(rng, n)
+    if levels < 128:
+        ints = [x & ((1 << levels) - 1) for x in O.ints_from_blocks(tree)]
+        tree = O.blocks_from_ints(ints)
+    bi = rng.integers(0, E, size=n, dtype=np.int32)
+    vcws = [[_rand_value(rng, vt) for _ in range(E)] for _ in range(num_keys)]
+    seeds_in = _rand_blocks(rng, n) if from_partials else None
+    ctrl_in = rng.integers(0, 2, size=n, dtype=np.uint8) if from_partials else None
+    want = []
+    for k in range(num_keys):
+        sl = slice(k * ppk, (k + 1) * ppk)
+        if from_partials:
+            s0, c0 = seeds_in[sl], ctrl_in[sl]
+        else:
+            s0 = np.repeat(key_seed[k:k + 1], ppk, axis=0)
+            c0 = np.full(ppk, party[k], np.uint8)
+        s, c = O.evaluate_seeds(s0, c0, tree[sl], cws[k * levels:(k + 1) * levels],
+                                cl[k * levels:(k + 1) * levels], cr[k * levels:(k + 1) * levels])
+        want.append(O.hash_select_correct(vt, s, c, b, bi[sl], vcws[k], int(party[k])))
+    want = np.concatenate(want)
+    import torch
+    flat_vcw = O._leaf_array([e for v in vcws for e in v])
+    got = hip.eval_points(n, ppk, levels, hip.to_device_blocks(key_seed), hip.to_device_u8(party),
+                          hip.to_device_blocks(tree), torch.from_numpy(bi).cuda(),
+                          hip.to_device_blocks(cws), hip.to_device_u8(cl), hip.to_device_u8(cr),
+                          (O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE), _desc(hip, vt, b),
+                          hip.to_device_blocks(flat_vcw),
+                          seeds_in=hip.to_device_blocks(seeds_in) if from_partials else None,
+                          ctrl_in=hip.to_device_u8(ctrl_in) if from_partials else None)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy()[: want.size].reshape(want.shape), want)
+
+
+@pytest.mark.parametrize("vt", FAST_TYPES + GENERIC_TYPES[:4] + GENERIC_TYPES[6:9], ids=str)
+def test_eval_points_single_key(hip, vt):
+    _points_case(hip, np.random.default_rng(3), vt, 1, 777, 20)
+
+
+@pytest.mark.parametrize("levels", [0, 1, 63, 64, 127])
+def test_eval_points_many_keys(hip, levels):
+    _points_case(hip, np.random.default_rng(levels), ("int", 64), 37, 64, levels)
+
+
+def test_eval_points_from_partials(hip):
+    _points_case(hip, np.random.default_rng(11), ("xor", 128), 5, 100, 12, from_partials=True)
