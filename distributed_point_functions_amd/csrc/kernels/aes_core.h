@@ -125,6 +125,67 @@ DPF_HD Block4 mmo_hash(Block4 x, const LK& lk, const RK& rk) {
   return Block4{e.w0 ^ s.w0, e.w1 ^ s.w1, e.w2 ^ s.w2, e.w3 ^ s.w3};
 }
 
+
+// Two independent encryptions interleaved round by round (instruction-level
+// parallelism: one chain's LDS latency hides under the other's VALU work).
+template <class LK, class RKA, class RKB>
+DPF_HD void encrypt2(Block4& sa, Block4& sb, const LK& lk, const RKA& ra, const RKB& rb) {
+  uint32_t a0 = sa.w0 ^ ra(0), a1 = sa.w1 ^ ra(1), a2 = sa.w2 ^ ra(2), a3 = sa.w3 ^ ra(3);
+  uint32_t b0 = sb.w0 ^ rb(0), b1 = sb.w1 ^ rb(1), b2 = sb.w2 ^ rb(2), b3 = sb.w3 ^ rb(3);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+  for (int r = 1; r < 10; ++r) {
+    uint32_t n0 = lk.xor3(lk.template lookup<0, 0>(a0), lk.template lookup<1, 1>(a1),
+                          lk.template lookup<2, 2>(a2));
+    uint32_t n1 = lk.xor3(lk.template lookup<0, 0>(a1), lk.template lookup<1, 1>(a2),
+                          lk.template lookup<2, 2>(a3));
+    uint32_t n2 = lk.xor3(lk.template lookup<0, 0>(a2), lk.template lookup<1, 1>(a3),
+                          lk.template lookup<2, 2>(a0));
+    uint32_t n3 = lk.xor3(lk.template lookup<0, 0>(a3), lk.template lookup<1, 1>(a0),
+                          lk.template lookup<2, 2>(a1));
+    uint32_t m0 = lk.xor3(lk.template lookup<0, 0>(b0), lk.template lookup<1, 1>(b1),
+                          lk.template lookup<2, 2>(b2));
+    uint32_t m1 = lk.xor3(lk.template lookup<0, 0>(b1), lk.template lookup<1, 1>(b2),
+                          lk.template lookup<2, 2>(b3));
+    uint32_t m2 = lk.xor3(lk.template lookup<0, 0>(b2), lk.template lookup<1, 1>(b3),
+                          lk.template lookup<2, 2>(b0));
+    uint32_t m3 = lk.xor3(lk.template lookup<0, 0>(b3), lk.template lookup<1, 1>(b0),
+                          lk.template lookup<2, 2>(b1));
+    n0 = lk.xor3(n0, lk.template lookup<3, 3>(a3), ra(4 * r + 0));
+    n1 = lk.xor3(n1, lk.template lookup<3, 3>(a0), ra(4 * r + 1));
+    n2 = lk.xor3(n2, lk.template lookup<3, 3>(a1), ra(4 * r + 2));
+    n3 = lk.xor3(n3, lk.template lookup<3, 3>(a2), ra(4 * r + 3));
+    m0 = lk.xor3(m0, lk.template lookup<3, 3>(b3), rb(4 * r + 0));
+    m1 = lk.xor3(m1, lk.template lookup<3, 3>(b0), rb(4 * r + 1));
+    m2 = lk.xor3(m2, lk.template lookup<3, 3>(b1), rb(4 * r + 2));
+    m3 = lk.xor3(m3, lk.template lookup<3, 3>(b2), rb(4 * r + 3));
+    a0 = n0; a1 = n1; a2 = n2; a3 = n3;
+    b0 = m0; b1 = m1; b2 = m2; b3 = m3;
+  }
+  auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    uint32_t x = lk.template lookup<2, 0>(a), y = lk.template lookup<3, 1>(b);
+    uint32_t z = lk.template lookup<0, 2>(c), u = lk.template lookup<1, 3>(d);
+    uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
+    uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
+    return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ k;
+  };
+  sa = Block4{last(a0, a1, a2, a3, ra(40)), last(a1, a2, a3, a0, ra(41)),
+              last(a2, a3, a0, a1, ra(42)), last(a3, a0, a1, a2, ra(43))};
+  sb = Block4{last(b0, b1, b2, b3, rb(40)), last(b1, b2, b3, b0, rb(41)),
+              last(b2, b3, b0, b1, rb(42)), last(b3, b0, b1, b2, rb(43))};
+}
+
+// Two MMO hashes interleaved.
+template <class LK, class RKA, class RKB>
+DPF_HD void mmo_hash2(Block4& xa, Block4& xb, const LK& lk, const RKA& ra, const RKB& rb) {
+  Block4 sa = sigma(xa), sb = sigma(xb);
+  Block4 ea = sa, eb = sb;
+  encrypt2(ea, eb, lk, ra, rb);
+  xa = Block4{ea.w0 ^ sa.w0, ea.w1 ^ sa.w1, ea.w2 ^ sa.w2, ea.w3 ^ sa.w3};
+  xb = Block4{eb.w0 ^ sb.w0, eb.w1 ^ sb.w1, eb.w2 ^ sb.w2, eb.w3 ^ sb.w3};
+}
+
 // Host-side lookup over four plain 256-entry tables (unit checks only).
 struct HostLookup {
   uint32_t t[4][256];
