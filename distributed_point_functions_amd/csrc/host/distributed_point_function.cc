@@ -1,0 +1,747 @@
+// distributed_point_function.cc -- host orchestration of the DPF API.
+//
+// Semantics follow dpf/distributed_point_function.{h,cc} of the reference
+// (file:line references below: cc = .cc, h = .h).  The hot loops -- the
+// path walk (EvaluateSeeds), the subtree expansion (ExpandSeeds), leaf hashing
+// (HashExpandedSeeds) and the value-correction loop -- run on the GPU through
+// the C ABI of include/dpf_hip.h.  There is no CPU evaluation fallback: a
+// missing GPU surfaces as an INTERNAL status from the C ABI.
+#include "dpf/distributed_point_function.h"
+
+#include <sys/random.h>
+
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <unordered_map>
+
+#include "dpf_hip.h"
+
+namespace distributed_point_functions {
+
+namespace {
+
+// PRG keys (cc:32-42): first half of SHA256 of the constant names.
+constexpr uint128 kPrgKeyLeft = MakeUint128(0x5be037ccf6a03de5ULL, 0x935f08d0a5b6a2fdULL);
+constexpr uint128 kPrgKeyRight = MakeUint128(0xef94b6aedebb026cULL, 0xe2ea1fe0f66f4d0bULL);
+constexpr uint128 kPrgKeyValue = MakeUint128(0x05a5d1588c5423e3ULL, 0x46a31101b21d1c98ULL);
+
+Status FromHip(int code) {
+  if (code == 0) return OkStatus();
+  return Status(static_cast<StatusCode>(code), dpf_hip_last_error());
+}
+#define HIP_RETURN_IF_ERROR(expr) DPF_RETURN_IF_ERROR(FromHip(expr))
+
+dpf_block ToBlock(uint128 v) { return dpf_block{Uint128Low64(v), Uint128High64(v)}; }
+uint128 FromBlock(const dpf_block& b) { return MakeUint128(b.high, b.low); }
+uint128 FromProtoBlock(const Block& b) { return MakeUint128(b.high(), b.low()); }
+void SetProtoBlock(uint128 v, Block* b) {
+  b->set_high(Uint128High64(v));
+  b->set_low(Uint128Low64(v));
+}
+
+dpf_aes_key AesKey(uint128 k) {
+  dpf_aes_key r;
+  std::memcpy(r.bytes, &k, 16);
+  return r;
+}
+
+dpf_value_desc MakeDesc(const dpf_internal::FlatValueType& f, int blocks_needed) {
+  dpf_value_desc d;
+  std::memset(&d, 0, sizeof(d));
+  d.num_leaves = static_cast<int32_t>(f.leaves.size());
+  d.direct = f.direct ? 1 : 0;
+  d.elements_per_block = f.elements_per_block;
+  d.blocks_needed = blocks_needed;
+  for (size_t k = 0; k < f.leaves.size() && k < DPF_MAX_LEAVES; ++k) {
+    d.kind[k] = f.leaves[k].kind;
+    d.bits[k] = f.leaves[k].bits;
+    d.mod_low[k] = Uint128Low64(f.leaves[k].modulus);
+    d.mod_high[k] = Uint128High64(f.leaves[k].modulus);
+  }
+  return d;
+}
+
+struct U128Hash {
+  size_t operator()(uint128 v) const {
+    uint64_t x = Uint128Low64(v) * 0x9E3779B97F4A7C15ULL ^ Uint128High64(v);
+    x ^= x >> 29;
+    return static_cast<size_t>(x * 0xBF58476D1CE4E5B9ULL);
+  }
+};
+
+}  // namespace
+
+namespace dpf_internal {
+
+// A growable device allocation (C-ABI allocator), reused across calls.
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  ~DeviceBuffer() {
+    if (p_) dpf_hip_free(p_);
+  }
+  Status Reserve(size_t bytes) {
+    if (bytes <= cap_ && p_) return OkStatus();
+    if (p_) dpf_hip_free(p_);
+    p_ = nullptr;
+    cap_ = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    HIP_RETURN_IF_ERROR(dpf_hip_alloc(&p_, want));
+    cap_ = want;
+    return OkStatus();
+  }
+  // Copies on `stream` (ordered after earlier work on it) and waits.
+  template <typename T>
+  Status Upload(const T* data, size_t count, void* stream = nullptr) {
+    DPF_RETURN_IF_ERROR(Reserve(count * sizeof(T)));
+    return FromHip(dpf_hip_memcpy_h2d(p_, data, count * sizeof(T), stream));
+  }
+  void* get() const { return p_; }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p_); }
+
+ private:
+  void* p_ = nullptr;
+  size_t cap_ = 0;
+};
+
+class DeviceScratch {
+ public:
+  DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
+  DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;
+  DeviceBuffer key_seed, party, block_index;
+};
+
+}  // namespace dpf_internal
+
+// Expansion starts resident on the device.
+struct DistributedPointFunction::DeviceStart {
+  int64_t n = 0;
+  dpf_block* seeds = nullptr;
+  uint8_t* ctrl = nullptr;
+};
+
+DistributedPointFunction::DistributedPointFunction(
+    std::unique_ptr<dpf_internal::ProtoValidator> validator, std::vector<int> blocks_needed,
+    std::vector<dpf_internal::FlatValueType> flat, Aes128FixedKeyHash prg_left,
+    Aes128FixedKeyHash prg_right, Aes128FixedKeyHash prg_value)
+    : validator_(std::move(validator)),
+      blocks_needed_(std::move(blocks_needed)),
+      flat_(std::move(flat)),
+      prg_left_(prg_left),
+      prg_right_(prg_right),
+      prg_value_(prg_value),
+      scratch_(new dpf_internal::DeviceScratch()) {}
+
+DistributedPointFunction::~DistributedPointFunction() = default;
+
+StatusOr<std::unique_ptr<DistributedPointFunction>> DistributedPointFunction::Create(
+    const DpfParameters& parameters) {
+  return CreateIncremental(Span<const DpfParameters>(&parameters, 1));
+}
+
+StatusOr<std::unique_ptr<DistributedPointFunction>> DistributedPointFunction::CreateIncremental(
+    Span<const DpfParameters> parameters) {
+  // cc:566-617
+  DPF_ASSIGN_OR_RETURN(std::unique_ptr<dpf_internal::ProtoValidator> validator,
+                       dpf_internal::ProtoValidator::Create(parameters));
+  std::vector<int> blocks_needed(parameters.size());
+  std::vector<dpf_internal::FlatValueType> flat(parameters.size());
+  for (size_t i = 0; i < parameters.size(); ++i) {
+    DPF_ASSIGN_OR_RETURN(int bits, dpf_internal::BitsNeeded(parameters[i].value_type(),
+                                                             validator->parameters()[i].security_parameter()));
+    blocks_needed[i] = (bits + 127) / 128;
+    DPF_ASSIGN_OR_RETURN(flat[i], dpf_internal::Flatten(parameters[i].value_type()));
+  }
+  DPF_ASSIGN_OR_RETURN(Aes128FixedKeyHash prg_left, Aes128FixedKeyHash::Create(kPrgKeyLeft));
+  DPF_ASSIGN_OR_RETURN(Aes128FixedKeyHash prg_right, Aes128FixedKeyHash::Create(kPrgKeyRight));
+  DPF_ASSIGN_OR_RETURN(Aes128FixedKeyHash prg_value, Aes128FixedKeyHash::Create(kPrgKeyValue));
+  std::unique_ptr<DistributedPointFunction> dpf(new DistributedPointFunction(
+      std::move(validator), std::move(blocks_needed), std::move(flat), prg_left, prg_right,
+      prg_value));
+  // All unsigned integers are registered for backwards compatibility (cc:597-610).
+  DPF_RETURN_IF_ERROR(dpf->RegisterValueType<uint8_t>());
+  DPF_RETURN_IF_ERROR(dpf->RegisterValueType<uint16_t>());
+  DPF_RETURN_IF_ERROR(dpf->RegisterValueType<uint32_t>());
+  DPF_RETURN_IF_ERROR(dpf->RegisterValueType<uint64_t>());
+  DPF_RETURN_IF_ERROR(dpf->RegisterValueType<uint128>());
+  return dpf;
+}
+
+Status DistributedPointFunction::RegisterValueType(const ValueType& value_type) {
+  registered_types_.insert(dpf_internal::SerializeValueTypeDeterministically(value_type));
+  return OkStatus();
+}
+
+// ============================================================ key generation
+StatusOr<std::vector<Value>> DistributedPointFunction::ComputeValueCorrection(
+    int hierarchy_level, const uint128 seeds[2], uint128 alpha, const Value& beta,
+    bool invert) const {
+  // cc:63-99 and ComputeValueCorrectionFor<T> (value_type_helpers.h:597-631).
+  const int b = blocks_needed_[hierarchy_level];
+  std::vector<uint128> expanded(2 * b);
+  for (int j = 0; j < b; ++j) {
+    expanded[j] = seeds[0] + static_cast<uint128>(j);
+    expanded[b + j] = seeds[1] + static_cast<uint128>(j);
+  }
+  DPF_RETURN_IF_ERROR(prg_value_.Evaluate(MakeConstSpan(expanded), MakeSpan(expanded)));
+  const DpfParameters& params = parameters()[hierarchy_level];
+  const int block_index_bits = params.log_domain_size() - hierarchy_to_tree()[hierarchy_level];
+  const int index_in_block =
+      static_cast<int>(alpha & ((static_cast<uint128>(1) << block_index_bits) - 1));
+  // GetValueCorrectionFunction (cc:544-559)
+  if (!registered_types_.count(dpf_internal::SerializeValueTypeDeterministically(params.value_type())))
+    return FailedPreconditionError(
+        "No value correction function known for the following parameters:\n" +
+        params.DebugString() + "Did you call RegisterValueType<T>() with your value type?");
+  DPF_ASSIGN_OR_RETURN(std::vector<uint128> beta_leaves,
+                       dpf_internal::ValueToLeaves(params.value_type(), beta));
+  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
+  const int nl = static_cast<int>(f.leaves.size()), E = f.elements_per_block;
+  std::vector<uint128> a(E * nl), c(E * nl);
+  dpf_internal::ConvertBytesToLeaves(f, reinterpret_cast<const uint8_t*>(expanded.data()), a.data());
+  dpf_internal::ConvertBytesToLeaves(f, reinterpret_cast<const uint8_t*>(expanded.data() + b), c.data());
+  for (int k = 0; k < nl; ++k)
+    c[index_in_block * nl + k] = dpf_internal::LeafAdd(f.leaves[k], c[index_in_block * nl + k], beta_leaves[k]);
+  std::vector<Value> result;
+  result.reserve(E);
+  for (int e = 0; e < E; ++e) {
+    for (int k = 0; k < nl; ++k) {
+      uint128 v = dpf_internal::LeafSub(f.leaves[k], c[e * nl + k], a[e * nl + k]);
+      if (invert) v = dpf_internal::LeafNeg(f.leaves[k], v);
+      c[e * nl + k] = v;
+    }
+    int pos = 0;
+    result.push_back(dpf_internal::LeavesToValue(params.value_type(), c.data() + e * nl, &pos));
+  }
+  return result;
+}
+
+Status DistributedPointFunction::GenerateNext(int tree_level, uint128 alpha, Span<const Value> beta,
+                                              uint128 seeds[2], bool control_bits[2],
+                                              DpfKey keys[2]) const {
+  // cc:103-204 (line numbers of arXiv 2012.14884 Fig. 11 in the reference comments)
+  CorrectionWord* cw = keys[0].add_correction_words();
+  const auto& t2h = validator_->tree_to_hierarchy();
+  const int last_log = parameters().back().log_domain_size();
+  auto it = t2h.find(tree_level - 1);
+  if (it != t2h.end()) {
+    const int h = it->second;
+    uint128 alpha_prefix = 0;
+    const int shift = last_log - parameters()[h].log_domain_size();
+    if (shift < 128) alpha_prefix = alpha >> shift;
+    DPF_ASSIGN_OR_RETURN(std::vector<Value> vc,
+                         ComputeValueCorrection(h, seeds, alpha_prefix, beta[h], control_bits[1]));
+    for (Value& v : vc) *cw->add_value_correction() = std::move(v);
+  }
+  uint128 ex[2][2];
+  DPF_RETURN_IF_ERROR(prg_left_.Evaluate(Span<const uint128>(seeds, 2), Span<uint128>(ex[0], 2)));
+  DPF_RETURN_IF_ERROR(prg_right_.Evaluate(Span<const uint128>(seeds, 2), Span<uint128>(ex[1], 2)));
+  bool ec[2][2];
+  for (int br = 0; br < 2; ++br)
+    for (int p = 0; p < 2; ++p) {
+      ec[br][p] = (ex[br][p] & 1) != 0;
+      ex[br][p] &= ~static_cast<uint128>(1);
+    }
+  bool bit = false;
+  if (last_log - tree_level < 128) bit = ((alpha >> (last_log - tree_level)) & 1) != 0;
+  const int keep = bit ? 1 : 0, lose = bit ? 0 : 1;
+  const uint128 seed_correction = ex[lose][0] ^ ex[lose][1];
+  bool ccw[2];
+  ccw[0] = ec[0][0] ^ ec[0][1] ^ bit ^ 1;
+  ccw[1] = ec[1][0] ^ ec[1][1] ^ bit;
+  for (int p = 0; p < 2; ++p) {
+    seeds[p] = ex[keep][p] ^ (control_bits[p] ? seed_correction : 0);
+    control_bits[p] = ec[keep][p] ^ (control_bits[p] && ccw[keep]);
+  }
+  SetProtoBlock(seed_correction, cw->mutable_seed());
+  cw->set_control_left(ccw[0]);
+  cw->set_control_right(ccw[1]);
+  *keys[1].add_correction_words() = *cw;
+  return OkStatus();
+}
+
+StatusOr<std::pair<DpfKey, DpfKey>> DistributedPointFunction::GenerateKeysIncremental(
+    uint128 alpha, Span<const Value> beta) {
+  uint128 seeds[2];
+  // RAND_bytes in the reference (cc:656-658); getrandom(2) here.
+  if (getrandom(seeds, sizeof(seeds), 0) != static_cast<ssize_t>(sizeof(seeds)))
+    return InternalError("getrandom failed");
+  return GenerateKeysIncrementalWithSeeds(alpha, beta, seeds[0], seeds[1]);
+}
+
+StatusOr<std::pair<DpfKey, DpfKey>> DistributedPointFunction::GenerateKeysIncrementalWithSeeds(
+    uint128 alpha, Span<const Value> beta, uint128 seed_0, uint128 seed_1) {
+  // cc:619-687
+  const int H = static_cast<int>(parameters().size());
+  if (static_cast<int>(beta.size()) != H)
+    return InvalidArgumentError(
+        "`beta` has to have the same size as `parameters` passed at construction");
+  for (int i = 0; i < H; ++i) DPF_RETURN_IF_ERROR(validator_->ValidateValue(beta[i], i));
+  const int last_log = parameters().back().log_domain_size();
+  if (last_log < 128 && alpha >= (static_cast<uint128>(1) << last_log))
+    return InvalidArgumentError("`alpha` must be smaller than the output domain size");
+  DpfKey keys[2];
+  keys[0].set_party(0);
+  keys[1].set_party(1);
+  uint128 seeds[2] = {seed_0, seed_1};
+  SetProtoBlock(seeds[0], keys[0].mutable_seed());
+  SetProtoBlock(seeds[1], keys[1].mutable_seed());
+  bool control_bits[2] = {false, true};
+  const int T = tree_levels_needed();
+  keys[0].mutable_correction_words()->Reserve(T - 1);
+  keys[1].mutable_correction_words()->Reserve(T - 1);
+  for (int i = 1; i < T; ++i)
+    DPF_RETURN_IF_ERROR(GenerateNext(i, alpha, beta, seeds, control_bits, keys));
+  DPF_ASSIGN_OR_RETURN(std::vector<Value> last,
+                       ComputeValueCorrection(H - 1, seeds, alpha, beta.back(), control_bits[1]));
+  for (const Value& v : last) {
+    *keys[0].add_last_level_value_correction() = v;
+    *keys[1].add_last_level_value_correction() = v;
+  }
+  return std::make_pair(std::move(keys[0]), std::move(keys[1]));
+}
+
+StatusOr<EvaluationContext> DistributedPointFunction::CreateEvaluationContext(DpfKey key) const {
+  // cc:689-704
+  DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
+  EvaluationContext result;
+  for (const DpfParameters& p : parameters()) *result.add_parameters() = p;
+  *result.mutable_key() = std::move(key);
+  result.set_previous_hierarchy_level(-1);
+  return result;
+}
+
+// ============================================================ evaluation
+StatusOr<std::vector<uint128>> DistributedPointFunction::ValueCorrectionLeaves(const DpfKey& key,
+                                                                               int h) const {
+  // h:761-780 / h:883-902
+  const RepeatedField<Value>* vc;
+  if (h < static_cast<int>(parameters().size()) - 1) {
+    vc = &key.correction_words(hierarchy_to_tree()[h]).value_correction();
+  } else {
+    vc = &key.last_level_value_correction();
+  }
+  return dpf_internal::ValuesToLeafArray(parameters()[h].value_type(), flat_[h], *vc);
+}
+
+namespace {
+// Uploads the correction words [start, stop) of `key` to device buffers.
+Status UploadCorrectionWords(const DpfKey& key, int start, int stop,
+                             dpf_internal::DeviceScratch* s, void* stream) {
+  const int L = stop - start;
+  std::vector<dpf_block> seeds(std::max(L, 1));
+  std::vector<uint8_t> cl(std::max(L, 1)), cr(std::max(L, 1));
+  for (int j = 0; j < L; ++j) {
+    const CorrectionWord& cw = key.correction_words(start + j);
+    seeds[j] = ToBlock(FromProtoBlock(cw.seed()));
+    cl[j] = cw.control_left();
+    cr[j] = cw.control_right();
+  }
+  DPF_RETURN_IF_ERROR(s->cw_seed.Upload(seeds.data(), seeds.size(), stream));
+  DPF_RETURN_IF_ERROR(s->cw_left.Upload(cl.data(), cl.size(), stream));
+  return s->cw_right.Upload(cr.data(), cr.size(), stream);
+}
+}  // namespace
+
+Status DistributedPointFunction::ComputePartialEvaluations(
+    Span<const uint128> prefixes, int hierarchy_level, bool update_ctx, EvaluationContext& ctx,
+    DeviceStart* out, void* stream, const std::function<Status()>& before_device) const {
+  // cc:351-453
+  const int64_t n = static_cast<int64_t>(prefixes.size());
+  int start_level = hierarchy_to_tree()[ctx.partial_evaluations_level()];
+  const int stop_level = hierarchy_to_tree()[hierarchy_level];
+  std::vector<dpf_block> seeds(std::max<int64_t>(n, 1));
+  std::vector<uint8_t> ctrl(std::max<int64_t>(n, 1));
+  if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
+    std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> previous;
+    previous.reserve(ctx.partial_evaluations_size() * 2);
+    for (const PartialEvaluation& e : ctx.partial_evaluations()) {
+      auto value = std::make_pair(FromProtoBlock(e.seed()), e.control_bit());
+      auto [it, inserted] = previous.try_emplace(FromProtoBlock(e.prefix()), value);
+      if (!inserted && it->second != value)
+        return InvalidArgumentError(
+            "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
+    }
+    for (int64_t i = 0; i < n; ++i) {
+      uint128 previous_prefix = 0;
+      if (stop_level - start_level < 128) previous_prefix = prefixes[i] >> (stop_level - start_level);
+      auto it = previous.find(previous_prefix);
+      if (it == previous.end())
+        return InvalidArgumentError("Prefix not present in ctx.partial_evaluations at hierarchy level " +
+                                    std::to_string(hierarchy_level));
+      seeds[i] = ToBlock(it->second.first);
+      ctrl[i] = it->second.second;
+    }
+  } else {
+    const dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+    for (int64_t i = 0; i < n; ++i) {
+      seeds[i] = root;
+      ctrl[i] = static_cast<uint8_t>(ctx.key().party() & 1);
+    }
+    start_level = 0;
+  }
+  // Everything that can fail on the host is checked before device work starts.
+  if (before_device) DPF_RETURN_IF_ERROR(before_device());
+  auto* s = scratch_.get();
+  std::vector<dpf_block> paths(std::max<int64_t>(n, 1));
+  for (int64_t i = 0; i < n; ++i) paths[i] = ToBlock(prefixes[i]);
+  DPF_RETURN_IF_ERROR(s->path_seed.Upload(seeds.data(), seeds.size(), stream));
+  DPF_RETURN_IF_ERROR(s->path_ctrl.Upload(ctrl.data(), ctrl.size(), stream));
+  DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size(), stream));
+  DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), start_level, stop_level, s, stream));
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight);
+  HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(
+      n, stop_level - start_level, s->path_seed.as<dpf_block>(), s->path_ctrl.as<uint8_t>(),
+      s->paths.as<dpf_block>(), s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
+      s->cw_right.as<uint8_t>(), &kl, &kr, s->path_seed.as<dpf_block>(), s->path_ctrl.as<uint8_t>(),
+      stream));
+  ctx.clear_partial_evaluations();
+  if (update_ctx) {
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds.data(), s->path_seed.get(), n * sizeof(dpf_block), stream));
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(ctrl.data(), s->path_ctrl.get(), n, stream));
+    ctx.mutable_partial_evaluations()->Reserve(static_cast<int>(n));
+    for (int64_t i = 0; i < n; ++i) {
+      PartialEvaluation* e = ctx.add_partial_evaluations();
+      SetProtoBlock(prefixes[i], e->mutable_prefix());
+      SetProtoBlock(FromBlock(seeds[i]), e->mutable_seed());
+      e->set_control_bit(ctrl[i] != 0);
+    }
+  }
+  ctx.set_partial_evaluations_level(hierarchy_level);
+  out->n = n;
+  out->seeds = s->path_seed.as<dpf_block>();
+  out->ctrl = s->path_ctrl.as<uint8_t>();
+  return OkStatus();
+}
+
+StatusOr<int64_t> DistributedPointFunction::OutputElements(int hierarchy_level,
+                                                           int64_t num_prefixes,
+                                                           int previous_hierarchy_level) const {
+  const int prev_log =
+      num_prefixes == 0 ? 0 : parameters()[previous_hierarchy_level].log_domain_size();
+  const int log = parameters()[hierarchy_level].log_domain_size();
+  if (log - prev_log > 62)
+    return InvalidArgumentError(
+        "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
+  return std::max<int64_t>(num_prefixes, 1) << (log - prev_log);
+}
+
+Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<const uint128> prefixes,
+                                                   EvaluationContext& ctx,
+                                                   const ValueType* requested_type,
+                                                   void* device_out, int64_t capacity_bytes,
+                                                   void* stream, std::vector<uint8_t>* host_out,
+                                                   int64_t* num_elements) const {
+  // h:641-837
+  DPF_RETURN_IF_ERROR(validator_->ValidateEvaluationContext(ctx));
+  const int H = static_cast<int>(parameters().size());
+  if (hierarchy_level < 0 || hierarchy_level >= H)
+    return InvalidArgumentError(
+        "`hierarchy_level` must be non-negative and less than parameters_.size()");
+  if (requested_type) {
+    DPF_ASSIGN_OR_RETURN(bool eq, dpf_internal::ValueTypesAreEqual(
+                                      *requested_type, parameters()[hierarchy_level].value_type()));
+    if (!eq) return InvalidArgumentError("Value type T doesn't match parameters at `hierarchy_level`");
+  }
+  if (hierarchy_level <= ctx.previous_hierarchy_level())
+    return InvalidArgumentError(
+        "`hierarchy_level` must be greater than `ctx.previous_hierarchy_level`");
+  if ((ctx.previous_hierarchy_level() < 0) != prefixes.empty())
+    return InvalidArgumentError(
+        "`prefixes` must be empty if and only if this is the first call with `ctx`.");
+  int previous_log_domain_size = 0;
+  const int previous_hierarchy_level = ctx.previous_hierarchy_level();
+  if (!prefixes.empty()) {
+    previous_log_domain_size = parameters()[previous_hierarchy_level].log_domain_size();
+    for (uint128 prefix : prefixes) {
+      if (previous_log_domain_size < 128 &&
+          prefix >= (static_cast<uint128>(1) << previous_log_domain_size))
+        return InvalidArgumentError("Index " + Uint128ToString(prefix) +
+                                    " out of range for hierarchy level " +
+                                    std::to_string(previous_hierarchy_level));
+    }
+  }
+  const int log_domain_size = parameters()[hierarchy_level].log_domain_size();
+  if (log_domain_size - previous_log_domain_size > 62)
+    return InvalidArgumentError(
+        "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
+
+  // Unique tree indices of the prefixes, in first-seen order (h:718-742).
+  const int64_t num_prefixes = static_cast<int64_t>(prefixes.size());
+  std::vector<uint128> tree_indices;
+  std::vector<std::pair<int64_t, int>> prefix_map;
+  if (num_prefixes > 0) {
+    const int bib = parameters()[previous_hierarchy_level].log_domain_size() -
+                    hierarchy_to_tree()[previous_hierarchy_level];
+    std::unordered_map<uint128, int64_t, U128Hash> inverse;
+    inverse.reserve(num_prefixes * 2);
+    tree_indices.reserve(num_prefixes);
+    prefix_map.reserve(num_prefixes);
+    for (int64_t i = 0; i < num_prefixes; ++i) {
+      uint128 ti = prefixes[i] >> bib;
+      int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
+      auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
+      if (inserted) tree_indices.push_back(ti);
+      prefix_map.emplace_back(it->second, bi);
+    }
+  }
+
+  // ExpandAndUpdateContext (cc:455-498): starting seeds on the device.  The
+  // value correction of this level (h:761-780) is parsed before device work.
+  auto* s = scratch_.get();
+  std::vector<uint128> vcw;
+  auto parse_vcw = [&]() -> Status {
+    DPF_ASSIGN_OR_RETURN(vcw, ValueCorrectionLeaves(ctx.key(), hierarchy_level));
+    return OkStatus();
+  };
+  DeviceStart start;
+  int start_level = 0;
+  if (tree_indices.empty()) {
+    DPF_RETURN_IF_ERROR(parse_vcw());
+    dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+    uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
+    DPF_RETURN_IF_ERROR(s->start_seed.Upload(&root, 1, stream));
+    DPF_RETURN_IF_ERROR(s->start_ctrl.Upload(&party, 1, stream));
+    start.n = 1;
+    start.seeds = s->start_seed.as<dpf_block>();
+    start.ctrl = s->start_ctrl.as<uint8_t>();
+  } else {
+    const bool update_ctx = hierarchy_level < H - 1;
+    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(MakeConstSpan(tree_indices),
+                                                  previous_hierarchy_level, update_ctx, ctx,
+                                                  &start, stream, parse_vcw));
+    start_level = hierarchy_to_tree()[previous_hierarchy_level];
+  }
+  const int stop_level = hierarchy_to_tree()[hierarchy_level];
+  ctx.set_previous_hierarchy_level(hierarchy_level);
+  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
+  const int cepb = corrected_elements_per_block(hierarchy_level);
+  const int esz = f.packed_size;
+  const int L = stop_level - start_level;
+  const int64_t expansion = start.n << L;
+  const int64_t corrected = expansion * cepb;
+  const int64_t outputs_per_prefix = int64_t{1} << (log_domain_size - previous_log_domain_size);
+  const int64_t total = num_prefixes == 0 ? corrected : num_prefixes * outputs_per_prefix;
+  *num_elements = total;
+
+  std::vector<dpf_block> vcw_blocks(vcw.size());
+  for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
+  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw_blocks.data(), vcw_blocks.size(), stream));
+  DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), start_level, stop_level, s, stream));
+
+  // Is the gather (h:822-835) the identity?  Yes when every prefix maps to its
+  // own tree index in order and covers the whole expanded block range.
+  const int64_t blocks_per_tree_prefix = num_prefixes ? (expansion / start.n) : 0;
+  bool identity = true;
+  if (num_prefixes > 0) {
+    identity = (outputs_per_prefix == blocks_per_tree_prefix * cepb) &&
+               static_cast<int64_t>(tree_indices.size()) == num_prefixes;
+    for (int64_t i = 0; identity && i < num_prefixes; ++i)
+      identity = prefix_map[i].first == i && prefix_map[i].second == 0;
+  }
+  void* expand_out = nullptr;
+  if (device_out && identity) {
+    if (capacity_bytes < total * esz) return InvalidArgumentError("device output buffer too small");
+    expand_out = device_out;
+  } else {
+    DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(corrected) * esz));
+    expand_out = s->out.get();
+  }
+  const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  HIP_RETURN_IF_ERROR(dpf_hip_expand(start.n, start.seeds, start.ctrl, L, s->cw_seed.as<dpf_block>(),
+                                     s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr, &kv,
+                                     &desc, cepb, s->vcw.as<dpf_block>(), ctx.key().party() & 1,
+                                     expand_out, stream));
+  void* result = expand_out;
+  if (!identity) {
+    std::vector<int64_t> offsets(num_prefixes);
+    for (int64_t i = 0; i < num_prefixes; ++i)
+      offsets[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
+                   prefix_map[i].second * outputs_per_prefix;
+    DPF_RETURN_IF_ERROR(s->offsets.Upload(offsets.data(), offsets.size(), stream));
+    if (device_out) {
+      if (capacity_bytes < total * esz) return InvalidArgumentError("device output buffer too small");
+      result = device_out;
+    } else {
+      DPF_RETURN_IF_ERROR(s->gathered.Reserve(static_cast<size_t>(total) * esz));
+      result = s->gathered.get();
+    }
+    HIP_RETURN_IF_ERROR(dpf_hip_gather(num_prefixes, outputs_per_prefix, esz,
+                                       s->offsets.as<int64_t>(), expand_out, result, stream));
+  }
+  if (!device_out) {
+    host_out->resize(static_cast<size_t>(total) * esz);
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(host_out->data(), result, host_out->size(), stream));
+  }
+  return OkStatus();
+}
+
+StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateUntilPacked(
+    int hierarchy_level, Span<const uint128> prefixes, EvaluationContext& ctx,
+    const ValueType* requested_type) const {
+  std::vector<uint8_t> out;
+  int64_t n = 0;
+  DPF_RETURN_IF_ERROR(EvaluateUntilCore(hierarchy_level, prefixes, ctx, requested_type, nullptr, 0,
+                                        nullptr, &out, &n));
+  return out;
+}
+
+StatusOr<int64_t> DistributedPointFunction::EvaluateUntilToDevice(
+    int hierarchy_level, Span<const uint128> prefixes, EvaluationContext& ctx, void* device_out,
+    int64_t capacity_bytes, void* stream, const ValueType* requested_type) const {
+  if (!device_out) return InvalidArgumentError("device_out must not be null");
+  int64_t n = 0;
+  DPF_RETURN_IF_ERROR(EvaluateUntilCore(hierarchy_level, prefixes, ctx, requested_type, device_out,
+                                        capacity_bytes, stream, nullptr, &n));
+  return n;
+}
+
+StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
+    const DpfKey& key, int hierarchy_level, Span<const uint128> evaluation_points,
+    EvaluationContext* ctx, const ValueType* requested_type) const {
+  // h:839-1010
+  if (ctx != nullptr && &key != &ctx->key())
+    return InvalidArgumentError("`key` and `ctx->key()` must refer to the same object");
+  if (hierarchy_level < 0) return InvalidArgumentError("`hierarchy_level` must be non-negative");
+  if (hierarchy_level >= static_cast<int>(parameters().size()))
+    return InvalidArgumentError(
+        "`hierarchy_level` must be less than the number of parameters passed at construction");
+  if (requested_type) {
+    // EvaluateAt<T> converts with T; a mismatching T is reported like EvaluateUntil does.
+    DPF_ASSIGN_OR_RETURN(bool eq, dpf_internal::ValueTypesAreEqual(
+                                      *requested_type, parameters()[hierarchy_level].value_type()));
+    if (!eq) return InvalidArgumentError("Value type T doesn't match parameters at `hierarchy_level`");
+  }
+  const int64_t n = static_cast<int64_t>(evaluation_points.size());
+  const int log_domain_size = parameters()[hierarchy_level].log_domain_size();
+  const uint128 max_point =
+      log_domain_size < 128 ? (static_cast<uint128>(1) << log_domain_size) - 1 : Uint128Max();
+  for (int64_t i = 0; i < n; ++i)
+    if (evaluation_points[i] > max_point)
+      return InvalidArgumentError("`evaluation_points[" + std::to_string(i) +
+                                  "]` larger than the domain size at hierarchy level " +
+                                  std::to_string(hierarchy_level));
+  DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
+  if (n == 0) return std::vector<uint8_t>{};
+  DPF_ASSIGN_OR_RETURN(std::vector<uint128> vcw, ValueCorrectionLeaves(key, hierarchy_level));
+  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
+  const int E = f.elements_per_block;
+  const int bib = log_domain_size - hierarchy_to_tree()[hierarchy_level];
+  std::vector<uint128> tree_indices(evaluation_points.begin(), evaluation_points.end());
+  std::vector<int32_t> block_index(n, 0);
+  if (E > 1) {
+    for (int64_t i = 0; i < n; ++i) {
+      tree_indices[i] = evaluation_points[i] >> bib;
+      block_index[i] = static_cast<int32_t>(evaluation_points[i] & ((static_cast<uint128>(1) << bib) - 1));
+    }
+  }
+  auto* s = scratch_.get();
+  const int stop_level = hierarchy_to_tree()[hierarchy_level];
+  int start_level = 0;
+  DeviceStart start;
+  if (ctx) {
+    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(MakeConstSpan(tree_indices), hierarchy_level,
+                                                  /*update_ctx=*/true, *ctx, &start, nullptr,
+                                                  nullptr));
+    start_level = stop_level;
+  }
+  std::vector<dpf_block> paths(n);
+  for (int64_t i = 0; i < n; ++i) paths[i] = ToBlock(tree_indices[i]);
+  DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size()));
+  DPF_RETURN_IF_ERROR(s->block_index.Upload(block_index.data(), block_index.size()));
+  DPF_RETURN_IF_ERROR(UploadCorrectionWords(key, start_level, stop_level, s, nullptr));
+  std::vector<dpf_block> vcw_blocks(vcw.size());
+  for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
+  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw_blocks.data(), vcw_blocks.size()));
+  dpf_block root = ToBlock(FromProtoBlock(key.seed()));
+  uint8_t party = static_cast<uint8_t>(key.party() & 1);
+  DPF_RETURN_IF_ERROR(s->key_seed.Upload(&root, 1));
+  DPF_RETURN_IF_ERROR(s->party.Upload(&party, 1));
+  DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
+  const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  HIP_RETURN_IF_ERROR(dpf_hip_eval_points(
+      n, n, stop_level - start_level, s->key_seed.as<dpf_block>(), s->party.as<uint8_t>(),
+      ctx ? start.seeds : nullptr, ctx ? start.ctrl : nullptr, s->paths.as<dpf_block>(),
+      s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
+      s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc, s->vcw.as<dpf_block>(), s->out.get(),
+      nullptr));
+  std::vector<uint8_t> out(static_cast<size_t>(n) * f.packed_size);
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
+  if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
+  return out;
+}
+
+StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtBatchPacked(
+    Span<const DpfKey* const> keys, int hierarchy_level, Span<const uint128> points,
+    int64_t points_per_key) const {
+  if (hierarchy_level < 0 || hierarchy_level >= static_cast<int>(parameters().size()))
+    return InvalidArgumentError("`hierarchy_level` out of range");
+  const int64_t num_keys = static_cast<int64_t>(keys.size());
+  if (points_per_key < 1 || static_cast<int64_t>(points.size()) != num_keys * points_per_key)
+    return InvalidArgumentError("points.size() must equal keys.size() * points_per_key");
+  const int log_domain_size = parameters()[hierarchy_level].log_domain_size();
+  const uint128 max_point =
+      log_domain_size < 128 ? (static_cast<uint128>(1) << log_domain_size) - 1 : Uint128Max();
+  const int64_t n = static_cast<int64_t>(points.size());
+  for (int64_t i = 0; i < n; ++i)
+    if (points[i] > max_point)
+      return InvalidArgumentError("`evaluation_points[" + std::to_string(i) +
+                                  "]` larger than the domain size at hierarchy level " +
+                                  std::to_string(hierarchy_level));
+  if (n == 0) return std::vector<uint8_t>{};
+  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
+  const int E = f.elements_per_block, nl = static_cast<int>(f.leaves.size());
+  const int L = hierarchy_to_tree()[hierarchy_level];
+  const int bib = log_domain_size - L;
+  std::vector<dpf_block> seeds(num_keys), cw_seed(std::max<int64_t>(num_keys * L, 1));
+  std::vector<uint8_t> party(num_keys), cl(std::max<int64_t>(num_keys * L, 1)),
+      cr(std::max<int64_t>(num_keys * L, 1));
+  std::vector<dpf_block> vcw(num_keys * E * nl);
+  for (int64_t k = 0; k < num_keys; ++k) {
+    const DpfKey& key = *keys[k];
+    DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
+    seeds[k] = ToBlock(FromProtoBlock(key.seed()));
+    party[k] = static_cast<uint8_t>(key.party() & 1);
+    for (int j = 0; j < L; ++j) {
+      const CorrectionWord& cw = key.correction_words(j);
+      cw_seed[k * L + j] = ToBlock(FromProtoBlock(cw.seed()));
+      cl[k * L + j] = cw.control_left();
+      cr[k * L + j] = cw.control_right();
+    }
+    DPF_ASSIGN_OR_RETURN(std::vector<uint128> v, ValueCorrectionLeaves(key, hierarchy_level));
+    for (int i = 0; i < E * nl; ++i) vcw[k * E * nl + i] = ToBlock(v[i]);
+  }
+  std::vector<dpf_block> paths(n);
+  std::vector<int32_t> block_index(n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    paths[i] = ToBlock(E > 1 ? points[i] >> bib : points[i]);
+    if (E > 1) block_index[i] = static_cast<int32_t>(points[i] & ((static_cast<uint128>(1) << bib) - 1));
+  }
+  auto* s = scratch_.get();
+  DPF_RETURN_IF_ERROR(s->key_seed.Upload(seeds.data(), seeds.size()));
+  DPF_RETURN_IF_ERROR(s->party.Upload(party.data(), party.size()));
+  DPF_RETURN_IF_ERROR(s->cw_seed.Upload(cw_seed.data(), cw_seed.size()));
+  DPF_RETURN_IF_ERROR(s->cw_left.Upload(cl.data(), cl.size()));
+  DPF_RETURN_IF_ERROR(s->cw_right.Upload(cr.data(), cr.size()));
+  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw.data(), vcw.size()));
+  DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size()));
+  DPF_RETURN_IF_ERROR(s->block_index.Upload(block_index.data(), block_index.size()));
+  DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
+  const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  HIP_RETURN_IF_ERROR(dpf_hip_eval_points(
+      n, points_per_key, L, s->key_seed.as<dpf_block>(), s->party.as<uint8_t>(), nullptr, nullptr,
+      s->paths.as<dpf_block>(), s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(),
+      s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc,
+      s->vcw.as<dpf_block>(), s->out.get(), nullptr));
+  std::vector<uint8_t> out(static_cast<size_t>(n) * f.packed_size);
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
+  return out;
+}
+
+}  // namespace distributed_point_functions

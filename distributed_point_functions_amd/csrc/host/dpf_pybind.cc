@@ -1,0 +1,244 @@
+// dpf_pybind.cc -- Python binding of the host C++ DistributedPointFunction.
+// Protos cross the boundary as serialized bytes (the reference's wire format);
+// 128-bit integers as numpy uint64 arrays of shape (n, 2) = {low, high}.
+// Errors raise _dpf_host.StatusError("<code>|<message>"); the Python wrapper
+// (distributed_point_functions_amd/dpf.py) turns it into DpfStatusError.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "dpf/distributed_point_function.h"
+
+namespace py = pybind11;
+using namespace distributed_point_functions;
+
+namespace {
+
+struct StatusError : std::exception {
+  std::string what_;
+  explicit StatusError(const Status& s) : what_(std::to_string(s.raw_code()) + "|" + s.message()) {}
+  const char* what() const noexcept override { return what_.c_str(); }
+};
+
+void Check(const Status& s) {
+  if (!s.ok()) throw StatusError(s);
+}
+template <typename T>
+T Take(StatusOr<T> s) {
+  if (!s.ok()) throw StatusError(s.status());
+  return std::move(*s);
+}
+
+template <typename M>
+M Parse(const py::bytes& b) {
+  M m;
+  std::string s = b;
+  if (!m.ParseFromString(s)) throw StatusError(InvalidArgumentError("failed to parse proto bytes"));
+  return m;
+}
+template <typename M>
+py::bytes Ser(const M& m) {
+  return py::bytes(m.SerializeAsString());
+}
+
+std::vector<uint128> ToU128(const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& a) {
+  if (a.size() == 0) return {};
+  if (a.ndim() != 2 || a.shape(1) != 2) throw std::invalid_argument("expected uint64 array (n, 2)");
+  std::vector<uint128> r(a.shape(0));
+  auto v = a.unchecked<2>();
+  for (py::ssize_t i = 0; i < a.shape(0); ++i) r[i] = MakeUint128(v(i, 1), v(i, 0));
+  return r;
+}
+
+uint128 IntToU128(const py::int_& x) {
+  py::int_ mask((1ULL << 63) * 2 - 1);  // 2^64 - 1 via unsigned wrap
+  uint64_t lo = PyLong_AsUnsignedLongLongMask(x.ptr());
+  py::object hi_o = x.attr("__rshift__")(64);
+  uint64_t hi = PyLong_AsUnsignedLongLongMask(hi_o.ptr());
+  return MakeUint128(hi, lo);
+}
+
+py::array_t<uint8_t> ToArray(const std::vector<uint8_t>& v) {
+  py::array_t<uint8_t> a(static_cast<py::ssize_t>(v.size()));
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size());
+  return a;
+}
+
+std::unique_ptr<ValueType> OptType(const py::object& o) {
+  if (o.is_none()) return nullptr;
+  return std::make_unique<ValueType>(Parse<ValueType>(o.cast<py::bytes>()));
+}
+
+class PyDpf {
+ public:
+  static PyDpf CreateIncremental(const std::vector<py::bytes>& params) {
+    std::vector<DpfParameters> p;
+    for (const auto& b : params) p.push_back(Parse<DpfParameters>(b));
+    PyDpf r;
+    r.dpf_ = std::shared_ptr<DistributedPointFunction>(
+        Take(DistributedPointFunction::CreateIncremental(MakeConstSpan(p))).release());
+    return r;
+  }
+  void RegisterValueType(const py::bytes& vt) { Check(dpf_->RegisterValueType(Parse<ValueType>(vt))); }
+  py::tuple GenerateKeys(const py::int_& alpha, const std::vector<py::bytes>& betas) {
+    std::vector<Value> v;
+    for (const auto& b : betas) v.push_back(Parse<Value>(b));
+    auto keys = Take(dpf_->GenerateKeysIncremental(IntToU128(alpha), MakeConstSpan(v)));
+    return py::make_tuple(Ser(keys.first), Ser(keys.second));
+  }
+  py::tuple GenerateKeysWithSeeds(const py::int_& alpha, const std::vector<py::bytes>& betas,
+                                  const py::int_& s0, const py::int_& s1) {
+    std::vector<Value> v;
+    for (const auto& b : betas) v.push_back(Parse<Value>(b));
+    auto keys = Take(dpf_->GenerateKeysIncrementalWithSeeds(IntToU128(alpha), MakeConstSpan(v),
+                                                            IntToU128(s0), IntToU128(s1)));
+    return py::make_tuple(Ser(keys.first), Ser(keys.second));
+  }
+  py::bytes CreateEvaluationContext(const py::bytes& key) {
+    return Ser(Take(dpf_->CreateEvaluationContext(Parse<DpfKey>(key))));
+  }
+  py::tuple EvaluateUntil(int level, const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& prefixes,
+                          const py::bytes& ctx_bytes, const py::object& vt) {
+    EvaluationContext ctx = Parse<EvaluationContext>(ctx_bytes);
+    auto p = ToU128(prefixes);
+    auto t = OptType(vt);
+    std::vector<uint8_t> out;
+    {
+      py::gil_scoped_release nogil;
+      auto r = dpf_->EvaluateUntilPacked(level, MakeConstSpan(p), ctx, t.get());
+      if (!r.ok()) {
+        py::gil_scoped_acquire g;
+        throw StatusError(r.status());
+      }
+      out = std::move(*r);
+    }
+    return py::make_tuple(ToArray(out), Ser(ctx));
+  }
+  py::tuple EvaluateUntilToDevice(int level,
+                                  const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& prefixes,
+                                  const py::bytes& ctx_bytes, uintptr_t out_ptr, int64_t capacity,
+                                  uintptr_t stream, const py::object& vt) {
+    EvaluationContext ctx = Parse<EvaluationContext>(ctx_bytes);
+    auto p = ToU128(prefixes);
+    auto t = OptType(vt);
+    int64_t n = 0;
+    {
+      py::gil_scoped_release nogil;
+      auto r = dpf_->EvaluateUntilToDevice(level, MakeConstSpan(p), ctx, reinterpret_cast<void*>(out_ptr),
+                                           capacity, reinterpret_cast<void*>(stream), t.get());
+      if (!r.ok()) {
+        py::gil_scoped_acquire g;
+        throw StatusError(r.status());
+      }
+      n = *r;
+    }
+    return py::make_tuple(n, Ser(ctx));
+  }
+  py::array_t<uint8_t> EvaluateAt(const py::bytes& key_bytes, int level,
+                                  const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& points,
+                                  const py::object& vt) {
+    DpfKey key = Parse<DpfKey>(key_bytes);
+    auto p = ToU128(points);
+    auto t = OptType(vt);
+    return ToArray(Take(dpf_->EvaluateAtPacked(key, level, MakeConstSpan(p), nullptr, t.get())));
+  }
+  py::tuple EvaluateAtCtx(int level,
+                          const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& points,
+                          const py::bytes& ctx_bytes, const py::object& vt) {
+    EvaluationContext ctx = Parse<EvaluationContext>(ctx_bytes);
+    auto p = ToU128(points);
+    auto t = OptType(vt);
+    auto out = Take(dpf_->EvaluateAtPacked(ctx.key(), level, MakeConstSpan(p), &ctx, t.get()));
+    return py::make_tuple(ToArray(out), Ser(ctx));
+  }
+  py::array_t<uint8_t> EvaluateAtBatch(const std::vector<py::bytes>& keys, int level,
+                                       const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& points,
+                                       int64_t points_per_key) {
+    std::vector<DpfKey> k;
+    k.reserve(keys.size());
+    for (const auto& b : keys) k.push_back(Parse<DpfKey>(b));
+    std::vector<const DpfKey*> ptrs;
+    for (const auto& x : k) ptrs.push_back(&x);
+    auto p = ToU128(points);
+    return ToArray(Take(dpf_->EvaluateAtBatchPacked(MakeConstSpan(ptrs), level, MakeConstSpan(p),
+                                                    points_per_key)));
+  }
+  std::vector<py::bytes> Parameters() const {
+    std::vector<py::bytes> r;
+    for (const auto& p : dpf_->parameters()) r.push_back(Ser(p));
+    return r;
+  }
+  int TreeLevelsNeeded() const { return dpf_->tree_levels_needed(); }
+  std::vector<int> HierarchyToTree() const { return dpf_->hierarchy_to_tree(); }
+  int BlocksNeeded(int h) const { return dpf_->blocks_needed(h); }
+  int ElementsPerBlock(int h) const { return dpf_->flat_value_type(h).elements_per_block; }
+  int PackedSize(int h) const { return dpf_->flat_value_type(h).packed_size; }
+  int CorrectedElementsPerBlock(int h) const { return dpf_->corrected_elements_per_block(h); }
+  int64_t OutputElements(int h, int64_t n, int prev) const {
+    return Take(dpf_->OutputElements(h, n, prev));
+  }
+
+ private:
+  std::shared_ptr<DistributedPointFunction> dpf_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_dpf_host, m) {
+  m.doc() = "Host C++ DistributedPointFunction (MI355X engine) -- serialized-proto binding";
+  py::register_exception<StatusError>(m, "StatusError");
+  py::class_<PyDpf>(m, "DistributedPointFunction")
+      .def_static("create_incremental", &PyDpf::CreateIncremental)
+      .def("register_value_type", &PyDpf::RegisterValueType)
+      .def("generate_keys_incremental", &PyDpf::GenerateKeys)
+      .def("generate_keys_incremental_with_seeds", &PyDpf::GenerateKeysWithSeeds)
+      .def("create_evaluation_context", &PyDpf::CreateEvaluationContext)
+      .def("evaluate_until", &PyDpf::EvaluateUntil)
+      .def("evaluate_until_to_device", &PyDpf::EvaluateUntilToDevice)
+      .def("evaluate_at", &PyDpf::EvaluateAt)
+      .def("evaluate_at_ctx", &PyDpf::EvaluateAtCtx)
+      .def("evaluate_at_batch", &PyDpf::EvaluateAtBatch)
+      .def("parameters", &PyDpf::Parameters)
+      .def("tree_levels_needed", &PyDpf::TreeLevelsNeeded)
+      .def("hierarchy_to_tree", &PyDpf::HierarchyToTree)
+      .def("blocks_needed", &PyDpf::BlocksNeeded)
+      .def("elements_per_block", &PyDpf::ElementsPerBlock)
+      .def("packed_size", &PyDpf::PackedSize)
+      .def("corrected_elements_per_block", &PyDpf::CorrectedElementsPerBlock)
+      .def("output_elements", &PyDpf::OutputElements);
+  m.def("bits_needed", [](const py::bytes& vt, double sec) {
+    return Take(dpf_internal::BitsNeeded(Parse<ValueType>(vt), sec));
+  });
+  m.def("value_types_are_equal", [](const py::bytes& a, const py::bytes& b) {
+    return Take(dpf_internal::ValueTypesAreEqual(Parse<ValueType>(a), Parse<ValueType>(b)));
+  });
+  m.def("roundtrip", [](const std::string& name, const py::bytes& b) -> py::bytes {
+    // Parses and re-serializes one message (wire-format conformance tests).
+    if (name == "DpfKey") return Ser(Parse<DpfKey>(b));
+    if (name == "EvaluationContext") return Ser(Parse<EvaluationContext>(b));
+    if (name == "DpfParameters") return Ser(Parse<DpfParameters>(b));
+    if (name == "Value") return Ser(Parse<Value>(b));
+    if (name == "ValueType") return Ser(Parse<ValueType>(b));
+    if (name == "CorrectionWord") return Ser(Parse<CorrectionWord>(b));
+    if (name == "PartialEvaluation") return Ser(Parse<PartialEvaluation>(b));
+    if (name == "Block") return Ser(Parse<Block>(b));
+    throw std::invalid_argument("unknown message " + name);
+  });
+  m.def("debug_string", [](const std::string& name, const py::bytes& b) -> std::string {
+    if (name == "DpfKey") return Parse<DpfKey>(b).DebugString();
+    if (name == "EvaluationContext") return Parse<EvaluationContext>(b).DebugString();
+    if (name == "ValueType") return Parse<ValueType>(b).DebugString();
+    if (name == "Value") return Parse<Value>(b).DebugString();
+    throw std::invalid_argument("unknown message " + name);
+  });
+  m.def("validate_context", [](const std::vector<py::bytes>& params, const py::bytes& ctx) {
+    std::vector<DpfParameters> p;
+    for (const auto& b : params) p.push_back(Parse<DpfParameters>(b));
+    auto v = Take(dpf_internal::ProtoValidator::Create(MakeConstSpan(p)));
+    Check(v->ValidateEvaluationContext(Parse<EvaluationContext>(ctx)));
+  });
+}

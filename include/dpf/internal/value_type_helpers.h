@@ -1,0 +1,226 @@
+// value_type_helpers.h -- value types of the DPF output groups.
+//
+// Restates the behaviour of the reference's dpf/internal/value_type_helpers.{h,cc}
+// in a form suited to a GPU engine: every ValueType is *flattened* into its
+// integer leaves (declaration order).  Flattening is exact for nested tuples:
+// DirectlyFromBytes reads leaves at consecutive offsets (h:415-428) and
+// SampleAndUpdateBytes updates after every leaf but the last (h:430-443).
+// Templates (ValueTypeHelper<T>) only map C++ values <-> leaves; all semantics
+// (validation messages, conversion, group ops) live in value_type_helpers.cc.
+#ifndef DPF_INTERNAL_VALUE_TYPE_HELPERS_H_
+#define DPF_INTERNAL_VALUE_TYPE_HELPERS_H_
+
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "dpf/distributed_point_function.pb.h"
+#include "dpf/int_mod_n.h"
+#include "dpf/status.h"
+#include "dpf/tuple.h"
+#include "dpf/uint128.h"
+#include "dpf/xor_wrapper.h"
+
+namespace distributed_point_functions {
+namespace dpf_internal {
+
+enum LeafKind { kLeafInt = 0, kLeafIntModN = 1, kLeafXor = 2 };
+
+struct LeafSpec {
+  int kind = kLeafInt;
+  int bits = 0;
+  uint128 modulus = 0;
+};
+
+// A ValueType flattened to its leaves.
+struct FlatValueType {
+  std::vector<LeafSpec> leaves;
+  bool direct = true;          // CanBeConvertedDirectly (no IntModN leaf), h:342-344
+  int total_bits = 0;          // TotalBitSize
+  int packed_size = 0;         // bytes of one packed element (sum of leaf bytes)
+  int elements_per_block = 1;  // ElementsPerBlock<T>(), h:508-520
+};
+
+// ---- free functions (value_type_helpers.cc) --------------------------------
+StatusOr<FlatValueType> Flatten(const ValueType& value_type);
+StatusOr<bool> ValueTypesAreEqual(const ValueType& lhs, const ValueType& rhs);
+StatusOr<int> BitsNeeded(const ValueType& value_type, double security_parameter);
+StatusOr<uint128> ValueIntegerToUint128(const Value::Integer& in);
+Value::Integer Uint128ToValueInteger(uint128 in);
+std::string SerializeValueTypeDeterministically(const ValueType& value_type);
+
+// IntModNBase (dpf/int_mod_n.cc).
+double IntModNSecurityLevel(int num_samples, uint128 modulus);
+Status IntModNCheckParameters(int num_samples, int base_integer_bitsize, uint128 modulus,
+                              double security_parameter);
+StatusOr<int> IntModNNumBytesRequired(int num_samples, int base_integer_bitsize, uint128 modulus,
+                                      double security_parameter);
+
+// FromValue for a runtime ValueType, with the reference's error messages.
+StatusOr<std::vector<uint128>> ValueToLeaves(const ValueType& type, const Value& value);
+// ToValue for a runtime ValueType from flattened leaves (advances *pos).
+Value LeavesToValue(const ValueType& type, const uint128* leaves, int* pos);
+// ValuesToArray (h:544-563): exactly ElementsPerBlock values -> E * num_leaves leaves.
+StatusOr<std::vector<uint128>> ValuesToLeafArray(const ValueType& type, const FlatValueType& flat,
+                                                 const RepeatedField<Value>& values);
+// ConvertBytesToArrayOf (h:569-589): bytes (blocks_needed * 16) -> E * num_leaves leaves.
+void ConvertBytesToLeaves(const FlatValueType& flat, const uint8_t* bytes, uint128* out);
+// Group operations on one leaf (int_mod_n.h, xor_wrapper.h, unsigned wrap-around).
+uint128 LeafAdd(const LeafSpec& s, uint128 a, uint128 b);
+uint128 LeafSub(const LeafSpec& s, uint128 a, uint128 b);
+uint128 LeafNeg(const LeafSpec& s, uint128 a);
+// Packed element bytes <-> leaves.
+void PackLeaves(const FlatValueType& flat, const uint128* leaves, uint8_t* out);
+void UnpackLeaves(const FlatValueType& flat, const uint8_t* in, uint128* leaves);
+
+// ---- templates --------------------------------------------------------------
+template <typename T>
+using is_unsigned_integer =
+    std::disjunction<std::is_same<T, uint8_t>, std::is_same<T, uint16_t>,
+                     std::is_same<T, uint32_t>, std::is_same<T, uint64_t>,
+                     std::is_same<T, uint128>>;
+
+template <typename T, typename = void>
+struct ValueTypeHelper {
+  static constexpr bool IsSupportedType() { return false; }
+};
+
+template <typename T>
+struct is_supported_type {
+  static constexpr bool value = ValueTypeHelper<T>::IsSupportedType();
+};
+template <typename T>
+constexpr bool is_supported_type_v = is_supported_type<T>::value;
+
+// Unsigned integers.
+template <typename T>
+struct ValueTypeHelper<T, std::enable_if_t<is_unsigned_integer<T>::value>> {
+  static constexpr bool IsSupportedType() { return true; }
+  static constexpr int kNumLeaves = 1;
+  static ValueType ToValueType() {
+    ValueType r;
+    r.mutable_integer()->set_bitsize(8 * sizeof(T));
+    return r;
+  }
+  static Value ToValue(T v) {
+    Value r;
+    *r.mutable_integer() = Uint128ToValueInteger(static_cast<uint128>(v));
+    return r;
+  }
+  static void ToLeaves(const T& v, uint128* out) { out[0] = static_cast<uint128>(v); }
+  static T FromLeaves(const uint128* in) { return static_cast<T>(in[0]); }
+};
+
+// IntModN.
+template <typename B, typename M, M kModulus>
+struct ValueTypeHelper<IntModNImpl<B, M, kModulus>, void> {
+  using Type = IntModNImpl<B, M, kModulus>;
+  static constexpr bool IsSupportedType() { return is_unsigned_integer<B>::value; }
+  static constexpr int kNumLeaves = 1;
+  static ValueType ToValueType() {
+    ValueType r;
+    r.mutable_int_mod_n()->mutable_base_integer()->set_bitsize(8 * sizeof(B));
+    *r.mutable_int_mod_n()->mutable_modulus() = Uint128ToValueInteger(static_cast<uint128>(kModulus));
+    return r;
+  }
+  static Value ToValue(const Type& v) {
+    Value r;
+    *r.mutable_int_mod_n() = Uint128ToValueInteger(static_cast<uint128>(v.value()));
+    return r;
+  }
+  static void ToLeaves(const Type& v, uint128* out) { out[0] = static_cast<uint128>(v.value()); }
+  static Type FromLeaves(const uint128* in) { return Type(static_cast<B>(in[0])); }
+};
+
+// XorWrapper.
+template <typename T>
+struct ValueTypeHelper<XorWrapper<T>, void> {
+  static constexpr bool IsSupportedType() { return is_unsigned_integer<T>::value; }
+  static constexpr int kNumLeaves = 1;
+  static ValueType ToValueType() {
+    ValueType r;
+    r.mutable_xor_wrapper()->set_bitsize(8 * sizeof(T));
+    return r;
+  }
+  static Value ToValue(const XorWrapper<T>& v) {
+    Value r;
+    *r.mutable_xor_wrapper() = Uint128ToValueInteger(static_cast<uint128>(v.value()));
+    return r;
+  }
+  static void ToLeaves(const XorWrapper<T>& v, uint128* out) {
+    out[0] = static_cast<uint128>(v.value());
+  }
+  static XorWrapper<T> FromLeaves(const uint128* in) {
+    return XorWrapper<T>(static_cast<T>(in[0]));
+  }
+};
+
+// Tuples.
+template <typename... E>
+struct ValueTypeHelper<Tuple<E...>, void> {
+  using Type = Tuple<E...>;
+  static constexpr bool IsSupportedType() { return (is_supported_type<E>::value && ...); }
+  static constexpr int kNumLeaves = (ValueTypeHelper<E>::kNumLeaves + ... + 0);
+  static ValueType ToValueType() {
+    ValueType r;
+    ValueType::Tuple* t = r.mutable_tuple();
+    ((*t->add_elements() = ValueTypeHelper<E>::ToValueType()), ...);
+    return r;
+  }
+  static Value ToValue(const Type& v) {
+    Value r;
+    Value::Tuple* t = r.mutable_tuple();
+    std::apply([&](const E&... e) { ((*t->add_elements() = ValueTypeHelper<E>::ToValue(e)), ...); },
+               v.value());
+    return r;
+  }
+  static void ToLeaves(const Type& v, uint128* out) {
+    int pos = 0;
+    std::apply([&](const E&... e) {
+      ((ValueTypeHelper<E>::ToLeaves(e, out + pos), pos += ValueTypeHelper<E>::kNumLeaves), ...);
+    }, v.value());
+  }
+  static Type FromLeaves(const uint128* in) {
+    int pos = 0;
+    // Braced init list: left-to-right evaluation.
+    return Type(typename Type::Base{Take<E>(in, pos)...});
+  }
+
+ private:
+  template <typename X>
+  static X Take(const uint128* in, int& pos) {
+    X x = ValueTypeHelper<X>::FromLeaves(in + pos);
+    pos += ValueTypeHelper<X>::kNumLeaves;
+    return x;
+  }
+};
+
+template <typename T>
+ValueType ToValueTypeImpl() { return ValueTypeHelper<T>::ToValueType(); }
+
+template <typename T>
+StatusOr<T> FromValueImpl(const Value& value) {
+  StatusOr<std::vector<uint128>> leaves = ValueToLeaves(ValueTypeHelper<T>::ToValueType(), value);
+  if (!leaves.ok()) return leaves.status();
+  return ValueTypeHelper<T>::FromLeaves(leaves->data());
+}
+
+// Unpacks n packed elements of T.
+template <typename T>
+std::vector<T> UnpackElements(const FlatValueType& flat, const uint8_t* data, int64_t n) {
+  std::vector<T> out;
+  out.reserve(n);
+  std::vector<uint128> leaves(flat.leaves.size());
+  for (int64_t i = 0; i < n; ++i) {
+    UnpackLeaves(flat, data + i * flat.packed_size, leaves.data());
+    out.push_back(ValueTypeHelper<T>::FromLeaves(leaves.data()));
+  }
+  return out;
+}
+
+}  // namespace dpf_internal
+}  // namespace distributed_point_functions
+
+#endif  // DPF_INTERNAL_VALUE_TYPE_HELPERS_H_
