@@ -600,6 +600,64 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilToDevice(
   return n;
 }
 
+StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
+    int hierarchy_level, int64_t shard, int64_t num_shards, EvaluationContext& ctx,
+    void* device_out, int64_t capacity_bytes, void* stream) const {
+  DPF_RETURN_IF_ERROR(validator_->ValidateEvaluationContext(ctx));
+  const int H = static_cast<int>(parameters().size());
+  if (hierarchy_level < 0 || hierarchy_level >= H)
+    return InvalidArgumentError(
+        "`hierarchy_level` must be non-negative and less than parameters_.size()");
+  if (ctx.previous_hierarchy_level() >= 0)
+    return InvalidArgumentError("sharded evaluation is only defined for the first call with `ctx`");
+  if (num_shards < 1 || (num_shards & (num_shards - 1)) || shard < 0 || shard >= num_shards)
+    return InvalidArgumentError("num_shards must be a power of two and 0 <= shard < num_shards");
+  int k = 0;
+  while ((int64_t{1} << k) < num_shards) ++k;
+  const int stop_level = hierarchy_to_tree()[hierarchy_level];
+  if (k > stop_level) return InvalidArgumentError("more shards than subtrees at this level");
+  const int log_domain_size = parameters()[hierarchy_level].log_domain_size();
+  if (log_domain_size - k > 62)
+    return InvalidArgumentError(
+        "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
+  DPF_ASSIGN_OR_RETURN(std::vector<uint128> vcw, ValueCorrectionLeaves(ctx.key(), hierarchy_level));
+  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
+  const int cepb = corrected_elements_per_block(hierarchy_level);
+  const int64_t total = (int64_t{1} << (stop_level - k)) * cepb;
+  if (!device_out || capacity_bytes < total * f.packed_size)
+    return InvalidArgumentError("device output buffer too small");
+  auto* s = scratch_.get();
+  // Walk the root to the shard's subtree root along the top k tree bits.
+  dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+  uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
+  dpf_block path = ToBlock(static_cast<uint128>(shard));
+  DPF_RETURN_IF_ERROR(s->start_seed.Upload(&root, 1, stream));
+  DPF_RETURN_IF_ERROR(s->start_ctrl.Upload(&party, 1, stream));
+  DPF_RETURN_IF_ERROR(s->paths.Upload(&path, 1, stream));
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  if (k > 0) {
+    DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), 0, k, s, stream));
+    HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(1, k, s->start_seed.as<dpf_block>(),
+                                           s->start_ctrl.as<uint8_t>(), s->paths.as<dpf_block>(),
+                                           s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
+                                           s->cw_right.as<uint8_t>(), &kl, &kr,
+                                           s->start_seed.as<dpf_block>(),
+                                           s->start_ctrl.as<uint8_t>(), stream));
+  }
+  std::vector<dpf_block> vcw_blocks(vcw.size());
+  for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
+  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw_blocks.data(), vcw_blocks.size(), stream));
+  DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), k, stop_level, s, stream));
+  const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
+  HIP_RETURN_IF_ERROR(dpf_hip_expand(1, s->start_seed.as<dpf_block>(), s->start_ctrl.as<uint8_t>(),
+                                     stop_level - k, s->cw_seed.as<dpf_block>(),
+                                     s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr,
+                                     &kv, &desc, cepb, s->vcw.as<dpf_block>(), party, device_out,
+                                     stream));
+  ctx.set_previous_hierarchy_level(hierarchy_level);
+  return total;
+}
+
 StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
     const DpfKey& key, int hierarchy_level, Span<const uint128> evaluation_points,
     EvaluationContext* ctx, const ValueType* requested_type) const {

@@ -138,6 +138,24 @@ class PyDpf {
     }
     return py::make_tuple(n, Ser(ctx));
   }
+  py::tuple EvaluateShardToDevice(int level, int64_t shard, int64_t num_shards,
+                                  const py::bytes& ctx_bytes, uintptr_t out_ptr, int64_t capacity,
+                                  uintptr_t stream) {
+    EvaluationContext ctx = Parse<EvaluationContext>(ctx_bytes);
+    int64_t n = 0;
+    {
+      py::gil_scoped_release nogil;
+      auto r = dpf_->EvaluateShardToDevice(level, shard, num_shards, ctx,
+                                           reinterpret_cast<void*>(out_ptr), capacity,
+                                           reinterpret_cast<void*>(stream));
+      if (!r.ok()) {
+        py::gil_scoped_acquire g;
+        throw StatusError(r.status());
+      }
+      n = *r;
+    }
+    return py::make_tuple(n, Ser(ctx));
+  }
   py::array_t<uint8_t> EvaluateAt(const py::bytes& key_bytes, int level,
                                   const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& points,
                                   const py::object& vt) {
@@ -199,6 +217,7 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("create_evaluation_context", &PyDpf::CreateEvaluationContext)
       .def("evaluate_until", &PyDpf::EvaluateUntil)
       .def("evaluate_until_to_device", &PyDpf::EvaluateUntilToDevice)
+      .def("evaluate_shard_to_device", &PyDpf::EvaluateShardToDevice)
       .def("evaluate_at", &PyDpf::EvaluateAt)
       .def("evaluate_at_ctx", &PyDpf::EvaluateAtCtx)
       .def("evaluate_at_batch", &PyDpf::EvaluateAtBatch)

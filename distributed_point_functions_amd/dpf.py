@@ -309,6 +309,17 @@ class DistributedPointFunction:
         ctx.ParseFromString(new_ctx)
         return n
 
+    def evaluate_shard_to_device(self, hierarchy_level: int, shard: int, num_shards: int,
+                                 ctx: pb.EvaluationContext, out, stream=None) -> int:
+        """Full-domain evaluation of one subtree-prefix shard into device tensor `out`."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        n, new_ctx = _call(self._impl.evaluate_shard_to_device, int(hierarchy_level), int(shard),
+                           int(num_shards), ctx.SerializeToString(), out.data_ptr(),
+                           out.numel() * out.element_size(), s.cuda_stream)
+        ctx.ParseFromString(new_ctx)
+        return n
+
     def evaluate_at_batch(self, keys: Sequence[pb.DpfKey], hierarchy_level: int,
                           points: Sequence[int], points_per_key: int, packed: bool = False):
         pts = points if isinstance(points, np.ndarray) else u128_array(points)

@@ -1,0 +1,53 @@
+"""Multi-GPU partition of a full-domain DPF level.
+
+The reference evaluates one key on one host (`EvaluateUntil`,
+dpf/distributed_point_function.h:785-835).  Full-domain evaluation is a tree
+expansion whose subtrees are independent, so N GPUs split it by *subtree
+prefix*: with N = 2^k ranks, rank r path-walks the top k tree levels along
+the bits of r (MSB first, as `EvaluateSeeds` walks a path,
+dpf/internal/evaluate_prg_hwy.cc:495-506) and expands the 2^(T-k)-leaf
+subtree below it (`DistributedPointFunction::EvaluateShardToDevice`).  Shard r
+covers output elements [r * n / N, (r + 1) * n / N): concatenating the shards
+in rank order is the reference's full-domain output.  There is no exchange on
+the data path; the only collective is the max-over-ranks of the step time.
+
+Weak scaling (bench.py): every rank keeps 2^log_per_gpu outputs, so the
+domain grows to 2^(log_per_gpu + k) with N.
+"""
+from __future__ import annotations
+
+
+def shard_bits(world: int) -> int:
+    """k = log2(world); the partition needs a power-of-two rank count."""
+    if world < 1 or world & (world - 1):
+        raise ValueError(f"world size must be a power of two, got {world}")
+    return world.bit_length() - 1
+
+
+def weak_scaling_log_domain(log_per_gpu: int, world: int) -> int:
+    """Domain size (log2) that gives each of `world` ranks 2^log_per_gpu outputs."""
+    return log_per_gpu + shard_bits(world)
+
+
+def shard_range(num_outputs: int, world: int, rank: int) -> tuple:
+    """[start, stop) of the output elements rank `rank` produces."""
+    shard_bits(world)
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    if num_outputs % world:
+        raise ValueError("output count not divisible by the shard count")
+    per = num_outputs // world
+    return rank * per, (rank + 1) * per
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """Max of a per-rank scalar (the step time) over the process group; the
+    identity without an initialised group."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64,
+                     device=device if device is not None else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -194,6 +194,15 @@ class DistributedPointFunction {
                                           EvaluationContext& ctx, void* device_out,
                                           int64_t capacity_bytes, void* stream,
                                           const ValueType* requested_type = nullptr) const;
+  // Multi-GPU sharding: the first (full-domain) evaluation of
+  // `hierarchy_level` restricted to shard `shard` of `num_shards` (a power of
+  // two): the outputs [shard * n / num_shards, (shard + 1) * n / num_shards) of
+  // EvaluateUntil(hierarchy_level, {}, ctx), i.e. the subtree under the top
+  // log2(num_shards) tree bits.  Writes packed elements to device memory and
+  // advances ctx like EvaluateUntil; returns the number of elements written.
+  StatusOr<int64_t> EvaluateShardToDevice(int hierarchy_level, int64_t shard, int64_t num_shards,
+                                          EvaluationContext& ctx, void* device_out,
+                                          int64_t capacity_bytes, void* stream) const;
   StatusOr<std::vector<uint8_t>> EvaluateAtPacked(const DpfKey& key, int hierarchy_level,
                                                   Span<const uint128> evaluation_points,
                                                   EvaluationContext* ctx,

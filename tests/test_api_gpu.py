@@ -306,3 +306,57 @@ def test_evaluate_at_batch_matches_per_key(vt):
     want = np.concatenate([dpf.evaluate_at(keys[k], 0, pts[k * ppk:(k + 1) * ppk], packed=True)
                            for k in range(9)])
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("levels,num_shards", [
+    ([(20, ("int", 64), 0)], 4),
+    ([(20, ("int", 64), 0)], 1),
+    ([(17, ("int", 32), 0)], 8),
+    ([(12, ("xor", 128), 0)], 16),
+    ([(10, ("tuple", [("int", 32), ("intmodn", 64, G.M64)]), 0)], 2),
+    ([(6, ("int", 16), 0), (15, ("int", 64), 0)], 4),
+], ids=str)
+def test_evaluate_shard_to_device_concatenates_to_full_domain(levels, num_shards):
+    """Weak-scaling shards (subtree prefixes of the top log2(N) tree levels)
+    concatenate to EvaluateUntil(h, {}) on a fresh context -- the multi-GPU
+    partition bench.py uses."""
+    import torch
+    dpf = E.params(levels)
+    k0, k1 = E.generate_keys(dpf, 0x5a5a % (1 << levels[0][0]),
+                             [[7] * len(O.leaves(l[1])) for l in levels], (11, 12))
+    h = len(levels) - 1
+    for key in (k0, k1):
+        # a fresh context evaluated straight to level h gives its full domain
+        want = dpf.evaluate_until(h, [], dpf.create_evaluation_context(key), packed=True)
+        per = want.size // num_shards
+        dev = torch.zeros(want.size, dtype=torch.uint8, device="cuda")
+        for s in range(num_shards):
+            ctx = dpf.create_evaluation_context(key)
+            n = dpf.evaluate_shard_to_device(h, s, num_shards, ctx, dev[s * per:(s + 1) * per])
+            assert n * want.shape[1] == per
+            assert ctx.previous_hierarchy_level == h
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy().reshape(want.shape), want)
+
+
+def test_evaluate_shard_to_device_errors():
+    import torch
+    dpf = E.params([(10, ("int", 64), 0)])
+    k0, _ = E.generate_keys(dpf, 3, [[1]], (1, 2))
+    dev = torch.zeros(1 << 13, dtype=torch.uint8, device="cuda")
+    for shard, num in [(0, 3), (4, 4), (-1, 2), (0, 0)]:
+        with pytest.raises(D.DpfStatusError) as e:
+            dpf.evaluate_shard_to_device(0, shard, num, dpf.create_evaluation_context(k0), dev)
+        assert e.value.code == 3
+    with pytest.raises(D.DpfStatusError, match="too small"):
+        dpf.evaluate_shard_to_device(0, 0, 1, dpf.create_evaluation_context(k0), dev[:100])
+    ctx = dpf.create_evaluation_context(k0)
+    dpf.evaluate_until(0, [], ctx)
+    with pytest.raises(D.DpfStatusError, match="fully evaluated"):
+        dpf.evaluate_shard_to_device(0, 0, 2, ctx, dev)
+    dpf2 = E.params([(5, ("int", 64), 0), (10, ("int", 64), 0)])
+    a, _ = E.generate_keys(dpf2, 3, [[1], [2]], (1, 2))
+    ctx = dpf2.create_evaluation_context(a)
+    dpf2.evaluate_until(0, [], ctx)
+    with pytest.raises(D.DpfStatusError, match="first call"):
+        dpf2.evaluate_shard_to_device(1, 0, 2, ctx, dev)

@@ -388,3 +388,27 @@ def test_fixture_context_value_correction_size_error():
                 pytest.skip("needs a GPU to reach the value-correction check")
             raise
     assert e.value.message == "values.size() (= 1) does not match ElementsPerBlock<T>() (= 4)"
+
+
+def test_evaluate_shard_argument_validation_before_device():
+    """EvaluateShardToDevice rejects bad shard arguments on the host, before
+    any device work (so these run without a GPU)."""
+    import torch
+    dpf = D.DistributedPointFunction.create(params([(10, ("int", 64), 0)])[0])
+    k0, _ = dpf.generate_keys_incremental(3, [D.to_value(D.integer_type(64), 1)], seeds=(1, 2))
+    buf = torch.zeros(1 << 13, dtype=torch.uint8)
+    for shard, num in [(0, 3), (4, 4), (-1, 2), (0, 0), (0, 1 << 10)]:
+        with pytest.raises(D.DpfStatusError) as e:
+            dpf.evaluate_shard_to_device(0, shard, num, dpf.create_evaluation_context(k0), buf,
+                                         stream=_NullStream())
+        assert e.value.code == 3, (shard, num, e.value.message)
+    with pytest.raises(D.DpfStatusError, match="too small"):
+        dpf.evaluate_shard_to_device(0, 0, 1, dpf.create_evaluation_context(k0), buf[:100],
+                                     stream=_NullStream())
+    with pytest.raises(D.DpfStatusError, match="hierarchy_level"):
+        dpf.evaluate_shard_to_device(1, 0, 1, dpf.create_evaluation_context(k0), buf,
+                                     stream=_NullStream())
+
+
+class _NullStream:
+    cuda_stream = 0
