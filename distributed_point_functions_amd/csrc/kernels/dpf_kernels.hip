@@ -543,35 +543,35 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(ExpandParams p, Leaf lea
       uint32_t bit = (uint32_t)((item >> (k0 - 1 - j)) & 1);
       path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
     }
-    // 2. depth-first over the subtree; stack[d] = node at depth d on the path.
-    Block4 st[kGMax + 1];
-    uint32_t tb = t;  // bit d = control bit of st[d]
-    st[0] = s;
+    // 2. depth-first over the subtree.  Every inner node is expanded into both
+    //    children at once (two interleaved hashes); the left child is descended
+    //    into and the right one parked in sib[d] until the walk returns to it,
+    //    so each node is hashed exactly once and always in a pair.
+    Block4 sib[kGMax + 1];
+    uint32_t tb = 0;  // bit d = control bit of sib[d]
     const int64_t leaf_base = item << S;
     for (int64_t g = 0; g < ngroups; ++g) {
-      int ds = 0;
-      uint32_t dir0 = 0;
+      Block4 node = s;
+      uint32_t nt = t;
+      int ds = 0;  // depth of `node` (wave-uniform)
       if (g != 0) {
-        ds = G - 1 - (int)__builtin_ctzll((unsigned long long)g);
-        dir0 = 1;
-      }
-      Block4 node = st[0];
-      uint32_t nt = tb & 1u;
+        ds = G - (int)__builtin_ctzll((unsigned long long)g);
 #pragma unroll
-      for (int d = 0; d < kGMax; ++d) {
-        if (d >= ds && d < G) {  // wave-uniform
-          uint32_t dir = (d == ds) ? dir0 : 0u;
-          Block4 c;
-          uint32_t ct;
-          child_step(lk, dir ? p.rkr.k : p.rkl.k, st[d], (tb >> d) & 1u, dir,
-                     lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d], c, ct);
-          st[d + 1] = c;
-          tb = (tb & ~(1u << (d + 1))) | (ct << (d + 1));
-        }
+        for (int d = 1; d <= kGMax; ++d)
+          if (d == ds) { node = sib[d]; nt = (tb >> d) & 1u; }
       }
+      for (int d = ds; d < G; ++d) {
+        Block4 c0, c1;
+        uint32_t t0, t1;
+        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d],
+                      c0, t0, c1, t1);
 #pragma unroll
-      for (int d = 1; d <= kGMax; ++d)
-        if (d == G) { node = st[d]; nt = (tb >> d) & 1u; }
+        for (int e = 1; e <= kGMax; ++e)
+          if (e == d + 1) sib[e] = c1;
+        tb = (tb & ~(1u << (d + 1))) | (t1 << (d + 1));
+        node = c0;
+        nt = t0;
+      }
       if (B == 0) {
         leaf.emit(lk, p.rkv.k, node, nt, leaf_base + g, p.out);
       } else {
