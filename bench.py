@@ -56,6 +56,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=32,
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
+    ap.add_argument("--workload", default="full_domain",
+                    choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum"],
+                    help="full_domain = BASELINE configs[1] (the headline); full_domain_u128 = "
+                         "configs[2] (2^31 uint128 outputs per GPU, 2^34 over 8 GPUs); "
+                         "evaluate_at(_sum) = configs[3] (2^20 keys x 2^10 points, log 128)")
+    ap.add_argument("--keys-log", type=int, default=20, help="evaluate_at: log2 keys (all ranks)")
+    ap.add_argument("--points-log", type=int, default=10, help="evaluate_at: log2 points per key")
     return ap.parse_args()
 
 
@@ -66,22 +73,29 @@ def tree_aes_per_launch(depth: int, blocks_needed: int = 1) -> int:
     return 2 * ((1 << depth) - 1) + blocks_needed * (1 << depth)
 
 
-def cpu_baseline(key, log_domain: int, chunks: int):
+def _int_of(v) -> int:
+    """Value.Integer -> int (uint64 or uint128 form)."""
+    if v.integer.WhichOneof("value") == "value_uint128":
+        return v.integer.value_uint128.high << 64 | v.integer.value_uint128.low
+    return int(v.integer.value_uint64)
+
+
+def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
     """The oracle (C restatement of dpf/distributed_point_function.cc:271-349,
     OpenSSL AES-NI in 64-block batches, one host thread) on a bounded sample of
     the SAME workload: `chunks` subtrees of 2^24 outputs of the benchmark key,
     each walked to its root (EvaluateSeeds) then expanded + hashed + corrected."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    P = O.OracleParams([(log_domain, ("int", 64), 0)])
-    sub = 23                                  # 2^23 blocks = 2^24 uint64 outputs per chunk
+    P = O.OracleParams([(log_domain, ("int", bits), 0)])
+    sub = 23 if bits == 64 else 24            # 2^24 outputs per chunk
     T = P.hierarchy_to_tree[0]
     top = T - sub
     # The product DpfKey (proto) restated as the oracle's key dict.
     k = {"seed": key.seed.high << 64 | key.seed.low, "party": key.party,
          "cws": [(c.seed.high << 64 | c.seed.low, int(c.control_left), int(c.control_right),
                   None) for c in key.correction_words],
-         "last_vc": [[int(v.integer.value_uint64)] for v in key.last_level_value_correction]}
+         "last_vc": [[_int_of(v)] for v in key.last_level_value_correction]}
     vcw = O._value_correction(P, k, 0)
     cs_top, cl_top, cr_top = O._cw_arrays(k, 0, top)
     cs, cl, cr = O._cw_arrays(k, top, T)
@@ -93,11 +107,11 @@ def cpu_baseline(key, log_domain: int, chunks: int):
                                       np.array([k["party"]], np.uint8),
                                       O.blocks_from_ints([c * stride]), cs_top, cl_top, cr_top)
         es, ec = O.expand_seeds(seed, ctrl, cs, cl, cr)
-        out = O.hash_correct(("int", 64), es, ec, 1, P.cepb(0), vcw, k["party"])
+        out = O.hash_correct(("int", bits), es, ec, 1, P.cepb(0), vcw, k["party"])
         leaves += out.shape[0]
     dt = time.perf_counter() - t0
     return {"value": leaves / dt, "unit": "leaves/s", "cores": 1, "kind": "port",
-            "sample": f"{chunks} subtrees x 2^24 uint64 outputs of the benchmark key "
+            "sample": f"{chunks} subtrees x 2^24 uint{bits} outputs of the benchmark key "
                       f"(2^{log_domain} domain): EvaluateSeeds to each subtree root, then "
                       f"ExpandSeeds+HashExpandedSeeds+correction; {dt:.1f} s on 1 host thread",
             "aes_blocks_per_s": chunks * (tree_aes_per_launch(sub) + top) / dt}
@@ -120,6 +134,10 @@ def profiled_traffic(leaves_per_launch: int):
 
 def main():
     args = parse()
+    if args.workload.startswith("evaluate_at"):
+        return main_evaluate_at(args)
+    if args.workload == "full_domain_u128" and args.log_domain == LOG_PER_GPU:
+        args.log_domain = 31
     import torch
     import torch.distributed as dist
     from distributed_point_functions_amd import dpf as D
@@ -140,20 +158,22 @@ def main():
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
 
+    bits = 128 if args.workload == "full_domain_u128" else 64
+    esz = bits // 8
     log_domain = S.weak_scaling_log_domain(args.log_domain, world)
     params = pb.DpfParameters()
     params.log_domain_size = log_domain
-    params.value_type.CopyFrom(D.integer_type(64))
+    params.value_type.CopyFrom(D.integer_type(bits))
     dpf = D.DistributedPointFunction.create(params)
     # Same key on every rank: root seeds injected (GenerateKeysIncrementalWithSeeds).
     alpha = 0x2545F4914F6CDD1D % (1 << log_domain)
-    beta = D.to_value(D.integer_type(64), 0xDEADBEEF)
+    beta = D.to_value(D.integer_type(bits), 0xDEADBEEF)
     key, _ = dpf.generate_keys_incremental(alpha, [beta], seeds=(0x243F6A8885A308D3,
                                                                  0x13198A2E03707344))
     ctx0 = dpf.create_evaluation_context(key)
     depth = dpf.hierarchy_to_tree()[0] - S.shard_bits(world)   # tree levels expanded per rank
     outputs_per_rank = 1 << args.log_domain
-    out = torch.empty(outputs_per_rank * 8, dtype=torch.uint8, device=dev)
+    out = torch.empty(outputs_per_rank * esz, dtype=torch.uint8, device=dev)
 
     def step(evs=None):
         ctx = pb.EvaluationContext()
@@ -185,15 +205,15 @@ def main():
 
     # Spot-check the last step's output (sum of the two parties' shares is beta
     # at alpha, 0 elsewhere) on a few positions of this rank's shard.
-    _check_shard(dpf, key, out, rank, world, outputs_per_rank, alpha)
+    _check_shard(dpf, key, out, rank, world, outputs_per_rank, alpha, bits)
 
     aes_per_launch = tree_aes_per_launch(depth)
     achieved = aes_per_launch / (kern_ms_max * 1e-3) / 1e9
-    bytes_per_launch = outputs_per_rank * 8
+    bytes_per_launch = outputs_per_rank * esz
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = profiled_traffic(outputs_per_rank)
+        tr = profiled_traffic(outputs_per_rank) if bits == 64 else None
         res = {
             "metric": METRIC,
             "value": total / elapsed,
@@ -205,12 +225,12 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u64",
+            "dtype": f"u{bits}",
             "data": "synthetic: one DpfKey from the product keygen with fixed root seeds",
             "config": {"workload": f"full-domain EvaluateUntil(0, {{}}) of one key, "
-                                   f"log_domain_size={log_domain}, uint64, 2^{args.log_domain} "
+                                   f"log_domain_size={log_domain}, uint{bits}, 2^{args.log_domain} "
                                    f"outputs per GPU",
-                       "log_domain_size": log_domain, "value_type": "uint64",
+                       "log_domain_size": log_domain, "value_type": f"uint{bits}",
                        "outputs_per_gpu": outputs_per_rank, "tree_levels_per_gpu": depth,
                        "parallelism": f"subtree-prefix x{world}"},
             "aes_blocks_per_s": aes_per_launch * world * args.steps / elapsed,
@@ -218,7 +238,7 @@ def main():
                          "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
                          "traffic": tr[0] if tr else None,
                          "traffic_source": tr[1] if tr else None,
-                         "kernel": KERNEL, "launch_ms": kern_ms_max,
+                         "kernel": KERNEL.replace("64", str(bits)), "launch_ms": kern_ms_max,
                          "algorithmic_aes_per_launch": aes_per_launch,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
             "roofline_hbm": {"bound": "hbm",
@@ -227,13 +247,199 @@ def main():
                              "frac": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS},
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(key, log_domain, args.cpu_chunks)
+            res["cpu_baseline"] = cpu_baseline(key, log_domain, args.cpu_chunks, bits)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def _check_shard(dpf, key, out, rank, world, n, alpha):
+EA_METRIC = ("batched EvaluateAt point evals/sec, 2^20 keys x 2^10 points each, log_domain 128, "
+             "uint64 (BASELINE configs[3]); AES blocks/s")
+EA_SUM_METRIC = ("aggregated EvaluateAt point evals/sec (sum over 2^20 keys at 2^10 shared points), "
+                 "log_domain 128, uint64 (BASELINE configs[3] aggregation variant)")
+
+
+def _oracle_key(key):
+    """A product DpfKey proto restated as the oracle's key dict (single level)."""
+    return {"seed": key.seed.high << 64 | key.seed.low, "party": key.party,
+            "cws": [(c.seed.high << 64 | c.seed.low, int(c.control_left), int(c.control_right),
+                     None) for c in key.correction_words],
+            "last_vc": [[_int_of(v)] for v in key.last_level_value_correction]}
+
+
+def cpu_baseline_points(dpf, batch, points_fn, keys: int, ppk: int):
+    """The oracle's EvaluateAtImpl (C restatement of distributed_point_function.h:
+    839-1010 over OpenSSL AES-NI in 64-block batches, one host thread) on a
+    bounded sample of the workload: `keys` keys of the batch x ppk points."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    P = O.OracleParams([(128, ("int", 64), 0)])
+    dt, done = 0.0, 0
+    while done < keys and dt < 10.0:         # bounded: ~10 s of CPU work
+        okey = _oracle_key(dpf.key_from_batch(batch, done))
+        pts = points_fn(done)
+        t0 = time.perf_counter()
+        O.evaluate_at(P, okey, 0, pts)
+        dt += time.perf_counter() - t0
+        done += 1
+    keys = done
+    n = keys * ppk
+    return {"value": n / dt, "unit": "points/s", "cores": 1, "kind": "port",
+            "sample": f"{keys} keys x {ppk} points of the benchmark batch (log 128, uint64): "
+                      f"EvaluateSeeds over 127 levels + value hash + correction; {dt:.1f} s on "
+                      f"1 host thread",
+            "aes_blocks_per_s": n * 128 / dt}
+
+
+def main_evaluate_at(args):
+    """EvaluateAt for 2^20 keys x 2^10 points on a 2^128
+    domain (uint64), keys split across ranks (DeviceKeyBatch rows [lo, hi)).
+    `evaluate_at`: independent points per key, outputs [key][point] stay in HBM.
+    `evaluate_at_sum`: one shared point set, sum over keys on the device, then
+    the per-rank partial sums are all-gathered (RCCL) and group-summed."""
+    import torch
+    import torch.distributed as dist
+    from distributed_point_functions_amd import dpf as D
+    from distributed_point_functions_amd import hip_abi as H
+    from distributed_point_functions_amd import proto as pb
+    from distributed_point_functions_amd import sharding as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    H.load(require_gpu=True)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    summed = args.workload == "evaluate_at_sum"
+
+    params = pb.DpfParameters()
+    params.log_domain_size = 128
+    params.value_type.CopyFrom(D.integer_type(64))
+    dpf = D.DistributedPointFunction.create(params)
+    n_keys, ppk = 1 << args.keys_log, 1 << args.points_log
+    lo, hi = S.key_range(n_keys, world, rank)
+    nk = hi - lo
+    # Keys: seeded alphas and root seeds for ALL keys (identical whatever the
+    # world size); each rank generates and uploads only its rows.
+    rng = np.random.default_rng(0xC0F4)
+    alphas = rng.integers(0, 2**64, size=(n_keys, 2), dtype=np.uint64)
+    seeds = rng.integers(0, 2**64, size=(2 * n_keys, 2), dtype=np.uint64)
+    beta = D.to_value(D.integer_type(64), 1)
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    b0, b1 = dpf.generate_key_batch(alphas[lo:hi], [beta], root_seeds=seeds[2 * lo:2 * hi],
+                                    threads=threads)
+    keygen_s = time.perf_counter() - t0
+    dbatch = dpf.upload_key_batch(b0, stream=stream)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    if summed:
+        shared = rng.integers(0, 2**64, size=(ppk, 2), dtype=np.uint64)
+        shared[:4] = alphas[:4]          # four points hit one client each (reconstruction check)
+        points = torch.from_numpy(shared.view(np.int64)).to(dev)
+        out = torch.empty(ppk * 8, dtype=torch.uint8, device=dev)
+    else:
+        points = torch.randint(-2**63, 2**63 - 1, (nk * ppk, 2), dtype=torch.int64, device=dev,
+                               generator=gen)
+        out = torch.empty(nk * ppk * 8, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        if summed:
+            dpf.evaluate_at_batch_sum_to_device(dbatch, 0, points, out, stream=stream)
+        else:
+            dpf.evaluate_at_batch_to_device(dbatch, 0, points, ppk, out, stream=stream)
+        if evs is not None:
+            evs[1].record(stream)
+        if summed and world > 1:
+            return S.aggregate_shares(dpf, 0, out, ppk)
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(H.Event(), H.Event()) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        total = step(evs[i])
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
+    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+
+    # Correctness spot checks outside the timed region.
+    if summed:
+        s0 = total if total is not None else out.cpu().numpy()
+        dpf.evaluate_at_batch_sum_to_device(dpf.upload_key_batch(b1, stream=stream), 0, points,
+                                            out, stream=stream)
+        s1 = S.aggregate_shares(dpf, 0, out, ppk) if world > 1 else out.cpu().numpy()
+        rec = (np.asarray(s0).view(np.uint64) + np.asarray(s1).view(np.uint64)).tolist()
+        if rec != [1, 1, 1, 1] + [0] * (ppk - 4):
+            raise SystemExit(f"rank {rank}: two-server reconstruction failed: {rec[:8]}")
+    else:
+        host_pts = points.view(-1, 2)
+        for k in (0, nk // 2, nk - 1):
+            pk = host_pts[k * ppk:(k + 1) * ppk].cpu().numpy().view(np.uint64)
+            pts = [int(a) | int(b) << 64 for a, b in pk[:64]]
+            want = dpf.evaluate_at(dpf.key_from_batch(b0, k), 0, pts)
+            got = out.view(torch.int64)[k * ppk:k * ppk + 64].cpu().numpy().view(np.uint64)
+            if not np.array_equal(got, want):
+                raise SystemExit(f"rank {rank}: batch output of key {lo + k} disagrees with EvaluateAt")
+
+    depth = dpf.hierarchy_to_tree()[0]                 # 127 path levels, + 1 value hash
+    aes_per_launch = nk * ppk * (depth + 1)
+    achieved = aes_per_launch / (kern_ms_max * 1e-3) / 1e9
+    if rank == 0:
+        res = {
+            "metric": EA_SUM_METRIC if summed else EA_METRIC,
+            "value": n_keys * ppk * args.steps / elapsed,
+            "unit": "points/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic: 2^20 key pairs from the product batched keygen (seeded alphas and "
+                    "root seeds, beta = 1), uniform random 128-bit points",
+            "config": {"workload": ("EvaluateAt summed over keys at shared points" if summed else
+                                    "EvaluateAt, independent points per key") +
+                                   f", {n_keys} keys x {ppk} points, log_domain_size=128, uint64",
+                       "keys": n_keys, "points_per_key": ppk, "log_domain_size": 128,
+                       "parallelism": f"key-batch x{world}"},
+            "aes_blocks_per_s": n_keys * ppk * (depth + 1) * args.steps / elapsed,
+            "keygen_s_rank0": keygen_s, "keygen_threads": threads,
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
+                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
+                         "traffic": None,
+                         "kernel": "eval_points_kernel<GenericLeaf, 64, true, true, %s>" %
+                                   ("true" if summed else "false"),
+                         "launch_ms": kern_ms_max, "algorithmic_aes_per_launch": aes_per_launch},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            host_pts = None if summed else points.view(-1, 2)
+
+            def pts_of(k):
+                if summed:
+                    return [int(a) | int(b) << 64 for a, b in shared.tolist()]
+                pk = host_pts[k * ppk:(k + 1) * ppk].cpu().numpy().view(np.uint64)
+                return [int(a) | int(b) << 64 for a, b in pk.tolist()]
+            res["cpu_baseline"] = cpu_baseline_points(dpf, b0, pts_of, nk, ppk)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _check_shard(dpf, key, out, rank, world, n, alpha, bits=64):
     """EvaluateAt on a handful of points of this shard must equal the device
     output (cheap, outside the timed region)."""
     import torch
@@ -241,11 +447,11 @@ def _check_shard(dpf, key, out, rank, world, n, alpha):
     local = sorted({0, n - 1, *map(int, rng.integers(0, n, size=6))})
     if alpha // n == rank:
         local.append(alpha % n)
-    words = out.view(torch.int64)
+    words = out.view(torch.int64).view(-1, bits // 64)
     pts = [rank * n + i for i in local]
-    want = np.asarray(dpf.evaluate_at(key, 0, pts), dtype=np.uint64)
-    got = np.array([int(words[i].item()) & (2**64 - 1) for i in local], dtype=np.uint64)
-    if not np.array_equal(got, want):
+    got_rows = words[torch.tensor(local, device=out.device)].cpu().numpy().view(np.uint64)
+    want_rows = dpf.evaluate_at(key, 0, pts, packed=True).view(np.uint64).reshape(got_rows.shape)
+    if not np.array_equal(got_rows, want_rows):
         raise SystemExit(f"rank {rank}: device output disagrees with EvaluateAt at {pts}")
 
 

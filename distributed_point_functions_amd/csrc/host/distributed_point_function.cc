@@ -16,105 +16,21 @@
 #include <unordered_map>
 
 #include "dpf_hip.h"
+#include "host_util.h"
 
 namespace distributed_point_functions {
 
-namespace {
-
-// PRG keys (cc:32-42): first half of SHA256 of the constant names.
-constexpr uint128 kPrgKeyLeft = MakeUint128(0x5be037ccf6a03de5ULL, 0x935f08d0a5b6a2fdULL);
-constexpr uint128 kPrgKeyRight = MakeUint128(0xef94b6aedebb026cULL, 0xe2ea1fe0f66f4d0bULL);
-constexpr uint128 kPrgKeyValue = MakeUint128(0x05a5d1588c5423e3ULL, 0x46a31101b21d1c98ULL);
-
-Status FromHip(int code) {
-  if (code == 0) return OkStatus();
-  return Status(static_cast<StatusCode>(code), dpf_hip_last_error());
-}
-#define HIP_RETURN_IF_ERROR(expr) DPF_RETURN_IF_ERROR(FromHip(expr))
-
-dpf_block ToBlock(uint128 v) { return dpf_block{Uint128Low64(v), Uint128High64(v)}; }
-uint128 FromBlock(const dpf_block& b) { return MakeUint128(b.high, b.low); }
-uint128 FromProtoBlock(const Block& b) { return MakeUint128(b.high(), b.low()); }
-void SetProtoBlock(uint128 v, Block* b) {
-  b->set_high(Uint128High64(v));
-  b->set_low(Uint128Low64(v));
-}
-
-dpf_aes_key AesKey(uint128 k) {
-  dpf_aes_key r;
-  std::memcpy(r.bytes, &k, 16);
-  return r;
-}
-
-dpf_value_desc MakeDesc(const dpf_internal::FlatValueType& f, int blocks_needed) {
-  dpf_value_desc d;
-  std::memset(&d, 0, sizeof(d));
-  d.num_leaves = static_cast<int32_t>(f.leaves.size());
-  d.direct = f.direct ? 1 : 0;
-  d.elements_per_block = f.elements_per_block;
-  d.blocks_needed = blocks_needed;
-  for (size_t k = 0; k < f.leaves.size() && k < DPF_MAX_LEAVES; ++k) {
-    d.kind[k] = f.leaves[k].kind;
-    d.bits[k] = f.leaves[k].bits;
-    d.mod_low[k] = Uint128Low64(f.leaves[k].modulus);
-    d.mod_high[k] = Uint128High64(f.leaves[k].modulus);
-  }
-  return d;
-}
-
-struct U128Hash {
-  size_t operator()(uint128 v) const {
-    uint64_t x = Uint128Low64(v) * 0x9E3779B97F4A7C15ULL ^ Uint128High64(v);
-    x ^= x >> 29;
-    return static_cast<size_t>(x * 0xBF58476D1CE4E5B9ULL);
-  }
-};
-
-}  // namespace
-
-namespace dpf_internal {
-
-// A growable device allocation (C-ABI allocator), reused across calls.
-class DeviceBuffer {
- public:
-  DeviceBuffer() = default;
-  DeviceBuffer(const DeviceBuffer&) = delete;
-  ~DeviceBuffer() {
-    if (p_) dpf_hip_free(p_);
-  }
-  Status Reserve(size_t bytes) {
-    if (bytes <= cap_ && p_) return OkStatus();
-    if (p_) dpf_hip_free(p_);
-    p_ = nullptr;
-    cap_ = 0;
-    size_t want = std::max<size_t>(bytes, 256);
-    HIP_RETURN_IF_ERROR(dpf_hip_alloc(&p_, want));
-    cap_ = want;
-    return OkStatus();
-  }
-  // Copies on `stream` (ordered after earlier work on it) and waits.
-  template <typename T>
-  Status Upload(const T* data, size_t count, void* stream = nullptr) {
-    DPF_RETURN_IF_ERROR(Reserve(count * sizeof(T)));
-    return FromHip(dpf_hip_memcpy_h2d(p_, data, count * sizeof(T), stream));
-  }
-  void* get() const { return p_; }
-  template <typename T>
-  T* as() const { return static_cast<T*>(p_); }
-
- private:
-  void* p_ = nullptr;
-  size_t cap_ = 0;
-};
-
-class DeviceScratch {
- public:
-  DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
-  DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;
-  DeviceBuffer key_seed, party, block_index;
-};
-
-}  // namespace dpf_internal
+using dpf_internal::AesKey;
+using dpf_internal::FromBlock;
+using dpf_internal::FromHip;
+using dpf_internal::FromProtoBlock;
+using dpf_internal::kPrgKeyLeft;
+using dpf_internal::kPrgKeyRight;
+using dpf_internal::kPrgKeyValue;
+using dpf_internal::MakeDesc;
+using dpf_internal::SetProtoBlock;
+using dpf_internal::ToBlock;
+using dpf_internal::U128Hash;
 
 // Expansion starts resident on the device.
 struct DistributedPointFunction::DeviceStart {
@@ -176,47 +92,101 @@ Status DistributedPointFunction::RegisterValueType(const ValueType& value_type) 
 }
 
 // ============================================================ key generation
-StatusOr<std::vector<Value>> DistributedPointFunction::ComputeValueCorrection(
-    int hierarchy_level, const uint128 seeds[2], uint128 alpha, const Value& beta,
+StatusOr<std::vector<uint128>> DistributedPointFunction::ComputeValueCorrectionLeaves(
+    int hierarchy_level, const uint128 seeds[2], uint128 alpha, Span<const uint128> beta_leaves,
     bool invert) const {
-  // cc:63-99 and ComputeValueCorrectionFor<T> (value_type_helpers.h:597-631).
+  // cc:63-99 and ComputeValueCorrectionFor<T> (value_type_helpers.h:597-631),
+  // on flattened leaves: E * num_leaves values, element-major.
   const int b = blocks_needed_[hierarchy_level];
-  std::vector<uint128> expanded(2 * b);
-  for (int j = 0; j < b; ++j) {
-    expanded[j] = seeds[0] + static_cast<uint128>(j);
-    expanded[b + j] = seeds[1] + static_cast<uint128>(j);
+  uint128 expanded[2 * 8];
+  std::vector<uint128> big;
+  uint128* ex = expanded;
+  if (b > 8) {
+    big.resize(2 * b);
+    ex = big.data();
   }
-  DPF_RETURN_IF_ERROR(prg_value_.Evaluate(MakeConstSpan(expanded), MakeSpan(expanded)));
+  for (int j = 0; j < b; ++j) {
+    ex[j] = seeds[0] + static_cast<uint128>(j);
+    ex[b + j] = seeds[1] + static_cast<uint128>(j);
+  }
+  DPF_RETURN_IF_ERROR(prg_value_.Evaluate(Span<const uint128>(ex, 2 * b), Span<uint128>(ex, 2 * b)));
   const DpfParameters& params = parameters()[hierarchy_level];
   const int block_index_bits = params.log_domain_size() - hierarchy_to_tree()[hierarchy_level];
   const int index_in_block =
       static_cast<int>(alpha & ((static_cast<uint128>(1) << block_index_bits) - 1));
+  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
+  const int nl = static_cast<int>(f.leaves.size()), E = f.elements_per_block;
+  std::vector<uint128> a(E * nl), c(E * nl);
+  dpf_internal::ConvertBytesToLeaves(f, reinterpret_cast<const uint8_t*>(ex), a.data());
+  dpf_internal::ConvertBytesToLeaves(f, reinterpret_cast<const uint8_t*>(ex + b), c.data());
+  for (int k = 0; k < nl; ++k)
+    c[index_in_block * nl + k] = dpf_internal::LeafAdd(f.leaves[k], c[index_in_block * nl + k], beta_leaves[k]);
+  for (int i = 0; i < E * nl; ++i) {
+    const auto& leaf = f.leaves[i % nl];
+    uint128 v = dpf_internal::LeafSub(leaf, c[i], a[i]);
+    c[i] = invert ? dpf_internal::LeafNeg(leaf, v) : v;
+  }
+  return c;
+}
+
+Status DistributedPointFunction::CheckValueCorrectionKnown(int hierarchy_level) const {
   // GetValueCorrectionFunction (cc:544-559)
+  const DpfParameters& params = parameters()[hierarchy_level];
   if (!registered_types_.count(dpf_internal::SerializeValueTypeDeterministically(params.value_type())))
     return FailedPreconditionError(
         "No value correction function known for the following parameters:\n" +
         params.DebugString() + "Did you call RegisterValueType<T>() with your value type?");
+  return OkStatus();
+}
+
+StatusOr<std::vector<Value>> DistributedPointFunction::ComputeValueCorrection(
+    int hierarchy_level, const uint128 seeds[2], uint128 alpha, const Value& beta,
+    bool invert) const {
+  const DpfParameters& params = parameters()[hierarchy_level];
+  DPF_RETURN_IF_ERROR(CheckValueCorrectionKnown(hierarchy_level));
   DPF_ASSIGN_OR_RETURN(std::vector<uint128> beta_leaves,
                        dpf_internal::ValueToLeaves(params.value_type(), beta));
-  const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
-  const int nl = static_cast<int>(f.leaves.size()), E = f.elements_per_block;
-  std::vector<uint128> a(E * nl), c(E * nl);
-  dpf_internal::ConvertBytesToLeaves(f, reinterpret_cast<const uint8_t*>(expanded.data()), a.data());
-  dpf_internal::ConvertBytesToLeaves(f, reinterpret_cast<const uint8_t*>(expanded.data() + b), c.data());
-  for (int k = 0; k < nl; ++k)
-    c[index_in_block * nl + k] = dpf_internal::LeafAdd(f.leaves[k], c[index_in_block * nl + k], beta_leaves[k]);
+  DPF_ASSIGN_OR_RETURN(std::vector<uint128> c,
+                       ComputeValueCorrectionLeaves(hierarchy_level, seeds, alpha,
+                                                    MakeConstSpan(beta_leaves), invert));
+  const int nl = static_cast<int>(flat_[hierarchy_level].leaves.size());
+  const int E = flat_[hierarchy_level].elements_per_block;
   std::vector<Value> result;
   result.reserve(E);
   for (int e = 0; e < E; ++e) {
-    for (int k = 0; k < nl; ++k) {
-      uint128 v = dpf_internal::LeafSub(f.leaves[k], c[e * nl + k], a[e * nl + k]);
-      if (invert) v = dpf_internal::LeafNeg(f.leaves[k], v);
-      c[e * nl + k] = v;
-    }
     int pos = 0;
     result.push_back(dpf_internal::LeavesToValue(params.value_type(), c.data() + e * nl, &pos));
   }
   return result;
+}
+
+Status DistributedPointFunction::GenerateNextCore(int tree_level, uint128 alpha, uint128 seeds[2],
+                                                  bool control_bits[2], uint128* seed_correction_out,
+                                                  bool ccw[2]) const {
+  // cc:138-201: expand both parties' seeds, keep the child on alpha's path,
+  // correct the other one away.
+  uint128 ex[2][2];
+  DPF_RETURN_IF_ERROR(prg_left_.Evaluate(Span<const uint128>(seeds, 2), Span<uint128>(ex[0], 2)));
+  DPF_RETURN_IF_ERROR(prg_right_.Evaluate(Span<const uint128>(seeds, 2), Span<uint128>(ex[1], 2)));
+  bool ec[2][2];
+  for (int br = 0; br < 2; ++br)
+    for (int p = 0; p < 2; ++p) {
+      ec[br][p] = (ex[br][p] & 1) != 0;
+      ex[br][p] &= ~static_cast<uint128>(1);
+    }
+  const int last_log = parameters().back().log_domain_size();
+  bool bit = false;
+  if (last_log - tree_level < 128) bit = ((alpha >> (last_log - tree_level)) & 1) != 0;
+  const int keep = bit ? 1 : 0, lose = bit ? 0 : 1;
+  const uint128 seed_correction = ex[lose][0] ^ ex[lose][1];
+  ccw[0] = ec[0][0] ^ ec[0][1] ^ bit ^ 1;
+  ccw[1] = ec[1][0] ^ ec[1][1] ^ bit;
+  for (int p = 0; p < 2; ++p) {
+    seeds[p] = ex[keep][p] ^ (control_bits[p] ? seed_correction : 0);
+    control_bits[p] = ec[keep][p] ^ (control_bits[p] && ccw[keep]);
+  }
+  *seed_correction_out = seed_correction;
+  return OkStatus();
 }
 
 Status DistributedPointFunction::GenerateNext(int tree_level, uint128 alpha, Span<const Value> beta,
@@ -236,26 +206,9 @@ Status DistributedPointFunction::GenerateNext(int tree_level, uint128 alpha, Spa
                          ComputeValueCorrection(h, seeds, alpha_prefix, beta[h], control_bits[1]));
     for (Value& v : vc) *cw->add_value_correction() = std::move(v);
   }
-  uint128 ex[2][2];
-  DPF_RETURN_IF_ERROR(prg_left_.Evaluate(Span<const uint128>(seeds, 2), Span<uint128>(ex[0], 2)));
-  DPF_RETURN_IF_ERROR(prg_right_.Evaluate(Span<const uint128>(seeds, 2), Span<uint128>(ex[1], 2)));
-  bool ec[2][2];
-  for (int br = 0; br < 2; ++br)
-    for (int p = 0; p < 2; ++p) {
-      ec[br][p] = (ex[br][p] & 1) != 0;
-      ex[br][p] &= ~static_cast<uint128>(1);
-    }
-  bool bit = false;
-  if (last_log - tree_level < 128) bit = ((alpha >> (last_log - tree_level)) & 1) != 0;
-  const int keep = bit ? 1 : 0, lose = bit ? 0 : 1;
-  const uint128 seed_correction = ex[lose][0] ^ ex[lose][1];
+  uint128 seed_correction;
   bool ccw[2];
-  ccw[0] = ec[0][0] ^ ec[0][1] ^ bit ^ 1;
-  ccw[1] = ec[1][0] ^ ec[1][1] ^ bit;
-  for (int p = 0; p < 2; ++p) {
-    seeds[p] = ex[keep][p] ^ (control_bits[p] ? seed_correction : 0);
-    control_bits[p] = ec[keep][p] ^ (control_bits[p] && ccw[keep]);
-  }
+  DPF_RETURN_IF_ERROR(GenerateNextCore(tree_level, alpha, seeds, control_bits, &seed_correction, ccw));
   SetProtoBlock(seed_correction, cw->mutable_seed());
   cw->set_control_left(ccw[0]);
   cw->set_control_right(ccw[1]);

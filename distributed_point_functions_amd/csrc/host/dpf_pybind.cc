@@ -73,6 +73,28 @@ std::unique_ptr<ValueType> OptType(const py::object& o) {
   return std::make_unique<ValueType>(Parse<ValueType>(o.cast<py::bytes>()));
 }
 
+struct PyKeyBatch {
+  std::shared_ptr<KeyBatch> b;
+  int64_t NumKeys() const { return b->num_keys; }
+  int NumLevels() const { return b->num_levels; }
+  py::array_t<uint64_t> Seeds() const {
+    py::array_t<uint64_t> a({static_cast<py::ssize_t>(b->num_keys), py::ssize_t{2}});
+    if (b->num_keys) std::memcpy(a.mutable_data(), b->seed.data(), b->num_keys * 16);
+    return a;
+  }
+  py::array_t<uint8_t> Party() const {
+    py::array_t<uint8_t> a(static_cast<py::ssize_t>(b->num_keys));
+    if (b->num_keys) std::memcpy(a.mutable_data(), b->party.data(), b->num_keys);
+    return a;
+  }
+};
+
+struct PyDeviceKeyBatch {
+  std::shared_ptr<DeviceKeyBatch> d;
+  int64_t NumKeys() const { return d->num_keys(); }
+  int64_t FirstKey() const { return d->first_key(); }
+};
+
 class PyDpf {
  public:
   static PyDpf CreateIncremental(const std::vector<py::bytes>& params) {
@@ -185,6 +207,67 @@ class PyDpf {
     return ToArray(Take(dpf_->EvaluateAtBatchPacked(MakeConstSpan(ptrs), level, MakeConstSpan(p),
                                                     points_per_key)));
   }
+  PyKeyBatch MakeKeyBatch(const std::vector<py::bytes>& keys) {
+    std::vector<DpfKey> k;
+    k.reserve(keys.size());
+    for (const auto& b : keys) k.push_back(Parse<DpfKey>(b));
+    std::vector<const DpfKey*> ptrs;
+    for (const auto& x : k) ptrs.push_back(&x);
+    return PyKeyBatch{std::make_shared<KeyBatch>(Take(dpf_->MakeKeyBatch(MakeConstSpan(ptrs))))};
+  }
+  py::bytes KeyFromBatch(const PyKeyBatch& b, int64_t k) { return Ser(Take(dpf_->KeyFromBatch(*b.b, k))); }
+  py::tuple GenerateKeyBatch(const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& alphas,
+                             const std::vector<py::bytes>& betas, const py::object& root_seeds,
+                             int threads) {
+    std::vector<Value> v;
+    for (const auto& b : betas) v.push_back(Parse<Value>(b));
+    auto a = ToU128(alphas);
+    std::vector<uint128> seeds;
+    if (!root_seeds.is_none())
+      seeds = ToU128(root_seeds.cast<py::array_t<uint64_t, py::array::c_style | py::array::forcecast>>());
+    std::pair<KeyBatch, KeyBatch> r;
+    {
+      py::gil_scoped_release nogil;
+      auto s = dpf_->GenerateKeyBatch(MakeConstSpan(a), MakeConstSpan(v), MakeConstSpan(seeds), threads);
+      if (!s.ok()) {
+        py::gil_scoped_acquire g;
+        throw StatusError(s.status());
+      }
+      r = std::move(*s);
+    }
+    return py::make_tuple(PyKeyBatch{std::make_shared<KeyBatch>(std::move(r.first))},
+                          PyKeyBatch{std::make_shared<KeyBatch>(std::move(r.second))});
+  }
+  int64_t EvaluateAtBatchToDevice(const PyDeviceKeyBatch& keys, int level, uintptr_t points,
+                                  int64_t points_per_key, bool shared, uintptr_t out,
+                                  int64_t capacity, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    auto r = dpf_->EvaluateAtBatchToDevice(*keys.d, level, reinterpret_cast<const void*>(points),
+                                           points_per_key, shared, reinterpret_cast<void*>(out),
+                                           capacity, reinterpret_cast<void*>(stream));
+    if (!r.ok()) {
+      py::gil_scoped_acquire g;
+      throw StatusError(r.status());
+    }
+    return *r;
+  }
+  void EvaluateAtBatchSumToDevice(const PyDeviceKeyBatch& keys, int level, uintptr_t points,
+                                  int64_t num_points, uintptr_t out, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    Status st = dpf_->EvaluateAtBatchSumToDevice(*keys.d, level, reinterpret_cast<const void*>(points),
+                                                 num_points, reinterpret_cast<void*>(out),
+                                                 reinterpret_cast<void*>(stream));
+    if (!st.ok()) {
+      py::gil_scoped_acquire g;
+      throw StatusError(st);
+    }
+  }
+  py::array_t<uint8_t> SumPackedShares(int level, const py::array_t<uint8_t, py::array::c_style>& shares,
+                                       int64_t num_shares, int64_t count) {
+    if (static_cast<int64_t>(shares.size()) != num_shares * count * dpf_->flat_value_type(level).packed_size)
+      throw StatusError(InvalidArgumentError("shares has the wrong size"));
+    return ToArray(Take(dpf_->SumPackedShares(level, shares.data(), num_shares, count)));
+  }
   std::vector<py::bytes> Parameters() const {
     std::vector<py::bytes> r;
     for (const auto& p : dpf_->parameters()) r.push_back(Ser(p));
@@ -209,6 +292,18 @@ class PyDpf {
 PYBIND11_MODULE(_dpf_host, m) {
   m.doc() = "Host C++ DistributedPointFunction (MI355X engine) -- serialized-proto binding";
   py::register_exception<StatusError>(m, "StatusError");
+  py::class_<PyDeviceKeyBatch>(m, "DeviceKeyBatch")
+      .def_property_readonly("num_keys", &PyDeviceKeyBatch::NumKeys)
+      .def_property_readonly("first_key", &PyDeviceKeyBatch::FirstKey);
+  py::class_<PyKeyBatch>(m, "KeyBatch")
+      .def_property_readonly("num_keys", &PyKeyBatch::NumKeys)
+      .def_property_readonly("num_levels", &PyKeyBatch::NumLevels)
+      .def("seeds", &PyKeyBatch::Seeds)
+      .def("party", &PyKeyBatch::Party)
+      .def("upload", [](const PyKeyBatch& b, int64_t begin, int64_t end, uintptr_t stream) {
+        auto d = Take(DeviceKeyBatch::Upload(*b.b, begin, end, reinterpret_cast<void*>(stream)));
+        return PyDeviceKeyBatch{std::shared_ptr<DeviceKeyBatch>(d.release())};
+      });
   py::class_<PyDpf>(m, "DistributedPointFunction")
       .def_static("create_incremental", &PyDpf::CreateIncremental)
       .def("register_value_type", &PyDpf::RegisterValueType)
@@ -221,6 +316,12 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("evaluate_at", &PyDpf::EvaluateAt)
       .def("evaluate_at_ctx", &PyDpf::EvaluateAtCtx)
       .def("evaluate_at_batch", &PyDpf::EvaluateAtBatch)
+      .def("make_key_batch", &PyDpf::MakeKeyBatch)
+      .def("key_from_batch", &PyDpf::KeyFromBatch)
+      .def("generate_key_batch", &PyDpf::GenerateKeyBatch)
+      .def("evaluate_at_batch_to_device", &PyDpf::EvaluateAtBatchToDevice)
+      .def("evaluate_at_batch_sum_to_device", &PyDpf::EvaluateAtBatchSumToDevice)
+      .def("sum_packed_shares", &PyDpf::SumPackedShares)
       .def("parameters", &PyDpf::Parameters)
       .def("tree_levels_needed", &PyDpf::TreeLevelsNeeded)
       .def("hierarchy_to_tree", &PyDpf::HierarchyToTree)

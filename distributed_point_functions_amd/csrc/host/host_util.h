@@ -1,0 +1,114 @@
+// host_util.h -- helpers shared by the host C++ sources: PRG keys, uint128 <->
+// dpf_block / proto Block conversion, C-ABI status mapping, the value-type
+// descriptor handed to the kernels, and reusable device allocations.
+#ifndef DPF_HOST_HOST_UTIL_H_
+#define DPF_HOST_HOST_UTIL_H_
+
+#include <algorithm>
+#include <cstring>
+
+#include "dpf/distributed_point_function.pb.h"
+#include "dpf/internal/value_type_helpers.h"
+#include "dpf/status.h"
+#include "dpf/uint128.h"
+#include "dpf_hip.h"
+
+namespace distributed_point_functions {
+namespace dpf_internal {
+
+// PRG keys (distributed_point_function.cc:32-42): first half of SHA256 of the
+// constant names.
+constexpr uint128 kPrgKeyLeft = MakeUint128(0x5be037ccf6a03de5ULL, 0x935f08d0a5b6a2fdULL);
+constexpr uint128 kPrgKeyRight = MakeUint128(0xef94b6aedebb026cULL, 0xe2ea1fe0f66f4d0bULL);
+constexpr uint128 kPrgKeyValue = MakeUint128(0x05a5d1588c5423e3ULL, 0x46a31101b21d1c98ULL);
+
+inline Status FromHip(int code) {
+  if (code == 0) return OkStatus();
+  return Status(static_cast<StatusCode>(code), dpf_hip_last_error());
+}
+#define HIP_RETURN_IF_ERROR(expr) DPF_RETURN_IF_ERROR(::distributed_point_functions::dpf_internal::FromHip(expr))
+
+inline dpf_block ToBlock(uint128 v) { return dpf_block{Uint128Low64(v), Uint128High64(v)}; }
+inline uint128 FromBlock(const dpf_block& b) { return MakeUint128(b.high, b.low); }
+inline uint128 FromProtoBlock(const Block& b) { return MakeUint128(b.high(), b.low()); }
+inline void SetProtoBlock(uint128 v, Block* b) {
+  b->set_high(Uint128High64(v));
+  b->set_low(Uint128Low64(v));
+}
+
+inline dpf_aes_key AesKey(uint128 k) {
+  dpf_aes_key r;
+  std::memcpy(r.bytes, &k, 16);
+  return r;
+}
+
+inline dpf_value_desc MakeDesc(const FlatValueType& f, int blocks_needed) {
+  dpf_value_desc d;
+  std::memset(&d, 0, sizeof(d));
+  d.num_leaves = static_cast<int32_t>(f.leaves.size());
+  d.direct = f.direct ? 1 : 0;
+  d.elements_per_block = f.elements_per_block;
+  d.blocks_needed = blocks_needed;
+  for (size_t k = 0; k < f.leaves.size() && k < DPF_MAX_LEAVES; ++k) {
+    d.kind[k] = f.leaves[k].kind;
+    d.bits[k] = f.leaves[k].bits;
+    d.mod_low[k] = Uint128Low64(f.leaves[k].modulus);
+    d.mod_high[k] = Uint128High64(f.leaves[k].modulus);
+  }
+  return d;
+}
+
+struct U128Hash {
+  size_t operator()(uint128 v) const {
+    uint64_t x = Uint128Low64(v) * 0x9E3779B97F4A7C15ULL ^ Uint128High64(v);
+    x ^= x >> 29;
+    return static_cast<size_t>(x * 0xBF58476D1CE4E5B9ULL);
+  }
+};
+
+// A growable device allocation (C-ABI allocator), reused across calls.
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  ~DeviceBuffer() {
+    if (p_) dpf_hip_free(p_);
+  }
+  Status Reserve(size_t bytes) {
+    if (bytes <= cap_ && p_) return OkStatus();
+    if (p_) dpf_hip_free(p_);
+    p_ = nullptr;
+    cap_ = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    HIP_RETURN_IF_ERROR(dpf_hip_alloc(&p_, want));
+    cap_ = want;
+    return OkStatus();
+  }
+  // Copies on `stream` (ordered after earlier work on it) and waits.
+  template <typename T>
+  Status Upload(const T* data, size_t count, void* stream = nullptr) {
+    DPF_RETURN_IF_ERROR(Reserve(count * sizeof(T)));
+    return FromHip(dpf_hip_memcpy_h2d(p_, data, count * sizeof(T), stream));
+  }
+  void* get() const { return p_; }
+  size_t capacity() const { return cap_; }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p_); }
+
+ private:
+  void* p_ = nullptr;
+  size_t cap_ = 0;
+};
+
+class DeviceScratch {
+ public:
+  DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
+  DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;
+  DeviceBuffer key_seed, party, block_index, workspace;
+};
+
+}  // namespace dpf_internal
+}  // namespace distributed_point_functions
+
+#endif  // DPF_HOST_HOST_UTIL_H_

@@ -586,10 +586,24 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(ExpandParams p, Leaf lea
   }
 }
 
+// Batched point evaluation (row a11).  Work item u covers
+// key k and the point PAIR (q, q + half) of that key, hashed as two
+// interleaved chains (ILP2).  With UNIFORM, half % 64 == 0, so all 64 lanes of
+// a wave share k: `k` is made wave-uniform and the key's correction words come
+// through scalar loads.  In sum mode (SUM) item u covers the pair for a chunk
+// of `chunk_keys` consecutive keys and accumulates the shares in the value
+// type's group before one wide atomic add per point.
 struct PointParams {
-  int64_t n;
-  int64_t points_per_key;
+  int64_t num_keys;
+  int64_t points_per_key;   // P
+  int64_t half;             // ceil(P / 2)
+  int64_t num_items;
+  int64_t chunk_keys;       // SUM: keys per item
+  int shared_points;        // tree_index/block_index indexed by point only
   int num_levels;
+  int cw_stride;            // correction words per key row (>= num_levels)
+  int bib;                  // block-index bits: tree_index holds raw domain points
+                            // (path = point >> bib, element = point & (2^bib - 1))
   const dpf_block* key_seed;
   const uint8_t* party;
   const dpf_block* seeds_in;
@@ -602,25 +616,56 @@ struct PointParams {
   const dpf_block* vcw;       // [key][E * num_leaves]
   int vcw_stride;             // E * num_leaves
   char* out;
+  unsigned long long* wide;   // SUM: [point][leaf][3] 192-bit exact sums
   int esz;
+  int xor_mode;               // fast leaves: XorWrapper
   RoundKeys rkl, rkd, rkv;
 };
 
-template <int BITS, bool XOR>
-__device__ __forceinline__ void point_store_fast(Block4 h, uint32_t t, int bi, dpf_block c,
-                                                 int party, char* o) {
-  // Element `bi` of the hashed block, corrected with its own correction value
-  // (distributed_point_function.h:993-1002).
-  unsigned __int128 x = ((unsigned __int128)h.w3 << 96) | ((unsigned __int128)h.w2 << 64) |
-                        ((unsigned __int128)h.w1 << 32) | h.w0;
-  unsigned __int128 cv = ((unsigned __int128)c.high << 64) | c.low;
+// Two path steps with per-lane directions, interleaved (evaluate_prg_hwy.cc:452-486).
+__device__ __forceinline__ void path_step2(const LdsLookup& lk, const RoundKeys& rkl,
+                                           const RoundKeys& rkd, Block4& s0, uint32_t& t0,
+                                           uint32_t b0, Block4& s1, uint32_t& t1, uint32_t b1,
+                                           uint4 cs, uint32_t cctl) {
+  Block4 h0 = s0, h1 = s1;
+  dpf_aes::mmo_hash2(h0, h1, lk, SelectRK{rkl.k, rkd.k, 0u - b0}, SelectRK{rkl.k, rkd.k, 0u - b1});
+  uint32_t m0 = 0u - t0, m1 = 0u - t1;
+  h0.w0 ^= cs.x & m0; h0.w1 ^= cs.y & m0; h0.w2 ^= cs.z & m0; h0.w3 ^= cs.w & m0;
+  h1.w0 ^= cs.x & m1; h1.w1 ^= cs.y & m1; h1.w2 ^= cs.z & m1; h1.w3 ^= cs.w & m1;
+  uint32_t n0 = (h0.w0 & 1u) ^ (t0 & ((cctl >> b0) & 1u));
+  uint32_t n1 = (h1.w0 & 1u) ^ (t1 & ((cctl >> b1) & 1u));
+  h0.w0 &= ~1u;
+  h1.w0 &= ~1u;
+  s0 = h0; t0 = n0;
+  s1 = h1; t1 = n1;
+}
+
+using u128 = unsigned __int128;
+
+__device__ __forceinline__ u128 block_u128(Block4 h) {
+  return ((u128)h.w3 << 96) | ((u128)h.w2 << 64) | ((u128)h.w1 << 32) | h.w0;
+}
+__device__ __forceinline__ u128 dpf_u128(dpf_block c) { return ((u128)c.high << 64) | c.low; }
+
+// Element `bi` of a directly converted integer block, corrected and negated
+// (distributed_point_function.h:993-1002; value_type_helpers.h:199-211).
+template <int BITS>
+__device__ __forceinline__ u128 fast_point_value(Block4 h, uint32_t t, int bi, u128 cv, int party,
+                                                 int xor_mode) {
+  u128 x = block_u128(h);
   if (BITS < 128) x >>= (bi * BITS) & 127;
-  if (XOR) {
+  if (xor_mode) {
     if (t) x ^= cv;
   } else {
     if (t) x += cv;
     if (party == 1) x = 0 - x;
   }
+  if (BITS < 128) x &= (((u128)1 << (BITS & 127)) - 1);
+  return x;
+}
+
+template <int BITS>
+__device__ __forceinline__ void store_bits(char* o, u128 x) {
   if (BITS == 128) {
     *reinterpret_cast<uint4*>(o) = make_uint4((uint32_t)x, (uint32_t)(x >> 32),
                                               (uint32_t)(x >> 64), (uint32_t)(x >> 96));
@@ -635,49 +680,206 @@ __device__ __forceinline__ void point_store_fast(Block4 h, uint32_t t, int bi, d
   }
 }
 
-// Fused EvaluateAt for many keys: path walk + hash + convert + correct.
-template <class Leaf, int BITS, bool XOR, bool FAST>
+// Adds v to a 192-bit little-endian accumulator held in three u64 words.
+// Exact under any interleaving of concurrent adders: each word's carry-out is
+// derived from the value the atomic returned.
+__device__ __forceinline__ void wide_add(unsigned long long* w, u128 v) {
+  unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
+  unsigned long long old = atomicAdd(w, lo);
+  unsigned long long c = (old + lo) < old ? 1ull : 0ull;
+  unsigned long long h = hi + c;
+  unsigned long long c2 = (h < hi) ? 1ull : 0ull;
+  if (h) {
+    unsigned long long old2 = atomicAdd(w + 1, h);
+    c2 += (old2 + h) < old2 ? 1ull : 0ull;
+  }
+  if (c2) atomicAdd(w + 2, c2);
+}
+__device__ __forceinline__ void wide_xor(unsigned long long* w, u128 v) {
+  atomicXor(w, (unsigned long long)v);
+  atomicXor(w + 1, (unsigned long long)(v >> 64));
+}
+
+// Packed-element conversion for the generic path: element `e` of the hashed
+// leaf, corrected and negated, as per-leaf values.
+__device__ void generic_point_values(const GenericLeaf& g, const LdsLookup& lk, const uint32_t* rkv,
+                                     Block4 seed, uint32_t t, int e, const dpf_block* vcw,
+                                     int party, u128* vals) {
+  char buf[16 * DPF_MAX_LEAVES];
+  GenericLeaf lf = g;
+  lf.vcw = vcw;
+  lf.party = party;
+  lf.convert_store(lk, rkv, seed, t, e, 1, buf);
+  int off = 0;
+  for (int k = 0; k < g.d.num_leaves; ++k) {
+    int lb = g.d.bits[k] >> 3;
+    vals[k] = GenericLeaf::load_le(reinterpret_cast<const uint8_t*>(buf) + off, lb);
+    off += lb;
+  }
+}
+
+__device__ __forceinline__ u128 leaf_group_add(const dpf_value_desc& d, int k, u128 a, u128 b) {
+  if (d.kind[k] == DPF_LEAF_XOR) return a ^ b;
+  if (d.kind[k] == DPF_LEAF_INTMODN) {
+    u128 n = ((u128)d.mod_high[k] << 64) | d.mod_low[k], c = n - b;
+    return a >= c ? a - c : n - c + a;
+  }
+  u128 m = d.bits[k] >= 128 ? ~(u128)0 : (((u128)1 << d.bits[k]) - 1);
+  return (a + b) & m;
+}
+
+template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM>
 __global__ __launch_bounds__(kBlock) void eval_points_kernel(PointParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
   const LdsLookup lk = make_lookup(lds);
   const int L = p.num_levels;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p.n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = i / p.points_per_key;
-    int party = p.party[k] & 1;
-    Block4 s;
-    uint32_t t;
-    if (p.seeds_in) {
-      s = load_block(p.seeds_in + i);
-      t = p.ctrl_in[i] & 1u;
-    } else {
-      s = load_block(p.key_seed + k);
-      t = (uint32_t)party;
+  const int64_t P = p.points_per_key, half = p.half;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    int64_t grp = u / half;
+    if (UNIFORM) grp = (int64_t)__builtin_amdgcn_readfirstlane((int)grp);
+    const int64_t q0 = u - grp * half;
+    const int64_t q1raw = q0 + half;
+    const bool has1 = q1raw < P;
+    const int64_t q1 = has1 ? q1raw : q0;
+    int64_t k_begin = grp, k_end = grp + 1;
+    if (SUM) {
+      k_begin = grp * p.chunk_keys;
+      k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
     }
-    Block4 path = load_block(p.tree_index + i);
-    const dpf_block* cws = p.cw_seed + k * L;
-    const uint8_t* cl = p.cw_left + k * L;
-    const uint8_t* cr = p.cw_right + k * L;
-    for (int j = 0; j < L; ++j) {
-      uint32_t bit = path_bit(path, L - 1 - j);
-      Block4 c = load_block(cws + j);
-      uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
-      path_step(lk, p.rkl, p.rkd, s, t, bit, make_uint4(c.w0, c.w1, c.w2, c.w3), cctl);
+    // Points are shared by all keys (sum mode always) or per key.
+    const int64_t pi0 = p.shared_points ? q0 : grp * P + q0;
+    const int64_t pi1 = p.shared_points ? q1 : grp * P + q1;
+    const Block4 path0 = load_block(p.tree_index + pi0);
+    const Block4 path1 = load_block(p.tree_index + pi1);
+    const int bb = p.bib;
+    const uint32_t bmask = (1u << bb) - 1u;
+    const int bi0 = p.block_index ? p.block_index[pi0] : (int)(path0.w0 & bmask);
+    const int bi1 = p.block_index ? p.block_index[pi1] : (int)(path1.w0 & bmask);
+    u128 acc0[FAST ? 1 : DPF_MAX_LEAVES], acc1[FAST ? 1 : DPF_MAX_LEAVES];
+    const int nl = FAST ? 1 : leaf.d.num_leaves;
+    for (int k = 0; k < nl; ++k) { acc0[k] = 0; acc1[k] = 0; }
+    for (int64_t k = k_begin; k < k_end; ++k) {
+      const int party = p.party[k] & 1;
+      Block4 s0, s1;
+      uint32_t t0, t1;
+      if (p.seeds_in) {
+        const int64_t o0 = k * P + q0, o1 = k * P + q1;
+        s0 = load_block(p.seeds_in + o0);
+        t0 = p.ctrl_in[o0] & 1u;
+        s1 = load_block(p.seeds_in + o1);
+        t1 = p.ctrl_in[o1] & 1u;
+      } else {
+        s0 = s1 = load_block(p.key_seed + k);
+        t0 = t1 = (uint32_t)party;
+      }
+      const dpf_block* cws = p.cw_seed + k * p.cw_stride;
+      const uint8_t* cl = p.cw_left + k * p.cw_stride;
+      const uint8_t* cr = p.cw_right + k * p.cw_stride;
+      for (int j = 0; j < L; ++j) {
+        const uint32_t b0 = path_bit(path0, L - 1 - j + bb), b1 = path_bit(path1, L - 1 - j + bb);
+        const dpf_block c = cws[j];
+        const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
+                                    (uint32_t)(c.high >> 32));
+        const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
+        path_step2(lk, p.rkl, p.rkd, s0, t0, b0, s1, t1, b1, cs, cctl);
+      }
+      const dpf_block* vcw = p.vcw + k * p.vcw_stride;
+      if constexpr (FAST) {
+        Block4 h0 = s0, h1 = s1;
+        dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+        const u128 v0 = fast_point_value<BITS>(h0, t0, bi0, dpf_u128(vcw[bi0]), party, p.xor_mode);
+        const u128 v1 = fast_point_value<BITS>(h1, t1, bi1, dpf_u128(vcw[bi1]), party, p.xor_mode);
+        if (SUM) {
+          acc0[0] = p.xor_mode ? (acc0[0] ^ v0) : (acc0[0] + v0);
+          acc1[0] = p.xor_mode ? (acc1[0] ^ v1) : (acc1[0] + v1);
+        } else {
+          store_bits<BITS>(p.out + (k * P + q0) * (int64_t)p.esz, v0);
+          if (has1) store_bits<BITS>(p.out + (k * P + q1) * (int64_t)p.esz, v1);
+        }
+      } else {
+        if (SUM) {
+          u128 v[DPF_MAX_LEAVES];
+          generic_point_values(leaf, lk, p.rkv.k, s0, t0, bi0, vcw, party, v);
+          for (int e = 0; e < nl; ++e) acc0[e] = leaf_group_add(leaf.d, e, acc0[e], v[e]);
+          generic_point_values(leaf, lk, p.rkv.k, s1, t1, bi1, vcw, party, v);
+          for (int e = 0; e < nl; ++e) acc1[e] = leaf_group_add(leaf.d, e, acc1[e], v[e]);
+        } else {
+          GenericLeaf lf = leaf;
+          lf.vcw = vcw;
+          lf.party = party;
+          lf.convert_store(lk, p.rkv.k, s0, t0, bi0, 1, p.out + (k * P + q0) * (int64_t)p.esz);
+          if (has1)
+            lf.convert_store(lk, p.rkv.k, s1, t1, bi1, 1, p.out + (k * P + q1) * (int64_t)p.esz);
+        }
+      }
     }
-    int bi = p.block_index ? p.block_index[i] : 0;
-    char* o = p.out + i * (int64_t)p.esz;
-    if constexpr (FAST) {
-      Block4 h = dpf_aes::mmo_hash(s, lk, UniformRK{p.rkv.k});
-      point_store_fast<BITS, XOR>(h, t, bi, p.vcw[k * p.vcw_stride + bi], party, o);
-    } else {
-      Leaf lf = leaf;
-      lf.vcw = p.vcw + k * p.vcw_stride;
-      lf.party = party;
-      lf.convert_store(lk, p.rkv.k, s, t, bi, 1, o);
+    if (SUM && k_begin < k_end) {
+      for (int e = 0; e < nl; ++e) {
+        const bool x = FAST ? p.xor_mode != 0 : leaf.d.kind[e] == DPF_LEAF_XOR;
+        unsigned long long* w0 = p.wide + (q0 * nl + e) * 3;
+        if (x) wide_xor(w0, acc0[e]); else wide_add(w0, acc0[e]);
+        if (has1) {
+          unsigned long long* w1 = p.wide + (q1 * nl + e) * 3;
+          if (x) wide_xor(w1, acc1[e]); else wide_add(w1, acc1[e]);
+        }
+      }
     }
   }
+}
+
+// Turns the 192-bit exact per-leaf sums into group elements and packs them:
+// plain integers keep the low `bits`, XorWrapper is already reduced, IntModN
+// takes the sum mod N (int_mod_n.h:116-120).
+__global__ void finalize_sums_kernel(int64_t num_points, dpf_value_desc d,
+                                     const unsigned long long* __restrict__ wide,
+                                     char* __restrict__ out) {
+  const int nl = d.num_leaves;
+  int esz = 0;
+  for (int k = 0; k < nl; ++k) esz += d.bits[k] >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < num_points;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    char* o = out + i * esz;
+    for (int k = 0; k < nl; ++k) {
+      const unsigned long long* w = wide + (i * nl + k) * 3;
+      u128 v = ((u128)w[1] << 64) | w[0];
+      if (d.kind[k] == DPF_LEAF_INTMODN) {
+        const u128 n = ((u128)d.mod_high[k] << 64) | d.mod_low[k];
+        // r = (w2 * 2^128 + v) mod n, one bit at a time (r < n throughout).
+        u128 r = 0;
+        for (int b = 191; b >= 0; --b) {
+          const unsigned bit = b >= 128 ? (unsigned)((w[2] >> (b - 128)) & 1)
+                                        : (unsigned)((v >> b) & 1);
+          r = (r >= n - r) ? r - (n - r) : r + r;  // 2r mod n
+          if (bit) r = (r >= n - 1) ? 0 : r + 1;   // +1 mod n
+        }
+        v = r;
+      }
+      const int lb = d.bits[k] >> 3;
+      for (int b = 0; b < lb; ++b) { o[b] = (char)(uint8_t)v; v >>= 8; }
+      o += lb;
+    }
+  }
+}
+
+// Counts points >= 2^log_domain_size (EvaluateAt's range check, h:861-874).
+__global__ void count_out_of_range_kernel(int64_t n, const dpf_block* __restrict__ pts, int log,
+                                          unsigned long long* __restrict__ bad) {
+  unsigned long long c = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const dpf_block b = pts[i];
+    bool out;
+    if (log >= 128) out = false;
+    else if (log >= 64) out = (b.high >> (log - 64)) != 0;
+    else out = b.high != 0 || (b.low >> log) != 0;
+    c += out ? 1 : 0;
+  }
+  // Wave-level reduction, one atomic per wave.
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, c);
 }
 
 __global__ void gather_kernel(int64_t rows, int64_t count, int elem_size,
@@ -784,11 +986,77 @@ int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf
   return launch_expand(p, FastIntLeaf<BITS, false>{vcw, E, party, store_bytes, {}}, s);
 }
 
-template <int BITS, bool XOR>
-int launch_points_fast(const PointParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((eval_points_kernel<GenericLeaf, BITS, XOR, true>),
-                     dim3(grid_for(p.n)), dim3(kBlock), 0, s, p, GenericLeaf{});
+template <class Leaf, int BITS, bool FAST, bool SUM>
+int launch_points_t(const PointParams& p, const Leaf& leaf, hipStream_t s) {
+  const dim3 grid(grid_for(p.num_items)), block(kBlock);
+  if (p.half % 64 == 0)
+    hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, true, SUM>), grid, block, 0, s, p, leaf);
+  else
+    hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, false, SUM>), grid, block, 0, s, p, leaf);
   HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+template <bool SUM>
+int launch_points(const PointParams& p, const dpf_value_desc* desc, const dpf_block* vcw,
+                  hipStream_t s) {
+  if (fast_int(desc)) {
+    switch (desc->bits[0]) {
+      case 8: return launch_points_t<GenericLeaf, 8, true, SUM>(p, GenericLeaf{}, s);
+      case 16: return launch_points_t<GenericLeaf, 16, true, SUM>(p, GenericLeaf{}, s);
+      case 32: return launch_points_t<GenericLeaf, 32, true, SUM>(p, GenericLeaf{}, s);
+      case 64: return launch_points_t<GenericLeaf, 64, true, SUM>(p, GenericLeaf{}, s);
+      default: return launch_points_t<GenericLeaf, 128, true, SUM>(p, GenericLeaf{}, s);
+    }
+  }
+  GenericLeaf g;
+  g.d = *desc;
+  g.vcw = vcw;
+  g.party = 0;
+  g.elements_per_leaf = 1;
+  g.esz = packed_size(desc);
+  return launch_points_t<GenericLeaf, 8, false, SUM>(p, g, s);
+}
+
+// Shared argument checks and parameter block of the two point entry points.
+int make_point_params(int64_t num_keys, int64_t points_per_key, int num_levels,
+                      const dpf_block* key_seed, const uint8_t* party, const dpf_block* seeds_in,
+                      const uint8_t* control_in, const dpf_block* tree_index,
+                      const int32_t* block_index, const dpf_block* cw_seed,
+                      const uint8_t* cw_left, const uint8_t* cw_right,
+                      const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                      const dpf_aes_key* key_value, const dpf_value_desc* desc,
+                      const dpf_block* value_correction, PointParams* p) {
+  int st = validate_desc(desc);
+  if (st) return st;
+  if (num_keys < 0 || points_per_key < 1 || num_levels < 0 || num_levels > 128)
+    return fail(kInvalidArgument, "num_keys, points_per_key or num_levels out of range");
+  if (!party || !tree_index || !key_left || !key_right || !key_value || !value_correction ||
+      (!seeds_in && !key_seed) || (seeds_in && !control_in) ||
+      (num_levels > 0 && (!cw_seed || !cw_left || !cw_right)))
+    return fail(kInvalidArgument, "NULL pointer");
+  memset(p, 0, sizeof(*p));
+  p->num_keys = num_keys;
+  p->points_per_key = points_per_key;
+  p->half = (points_per_key + 1) / 2;
+  p->num_levels = num_levels;
+  p->cw_stride = num_levels;
+  p->key_seed = key_seed;
+  p->party = party;
+  p->seeds_in = seeds_in;
+  p->ctrl_in = control_in;
+  p->tree_index = tree_index;
+  p->block_index = block_index;
+  p->cw_seed = cw_seed;
+  p->cw_left = cw_left;
+  p->cw_right = cw_right;
+  p->vcw = value_correction;
+  p->vcw_stride = desc->elements_per_block * desc->num_leaves;
+  p->esz = packed_size(desc);
+  p->xor_mode = desc->kind[0] == DPF_LEAF_XOR;
+  p->rkl = expand_key(key_left);
+  p->rkd = xor_keys(p->rkl, expand_key(key_right));
+  p->rkv = expand_key(key_value);
   return kOk;
 }
 
@@ -968,55 +1236,115 @@ int dpf_hip_eval_points(int64_t num_points, int64_t points_per_key, int num_leve
                         const dpf_aes_key* key_left, const dpf_aes_key* key_right,
                         const dpf_aes_key* key_value, const dpf_value_desc* desc,
                         const dpf_block* value_correction, void* out, void* stream) {
-  int st = validate_desc(desc);
-  if (st) return st;
-  if (num_points < 0 || points_per_key < 1 || num_levels < 0 || num_levels > 128)
-    return fail(kInvalidArgument, "num_points, points_per_key or num_levels out of range");
-  if (num_points == 0) return kOk;
-  if (!party || !tree_index || !key_left || !key_right || !key_value || !value_correction ||
-      !out || (!seeds_in && !key_seed) || (seeds_in && !control_in) ||
-      (num_levels > 0 && (!cw_seed || !cw_left || !cw_right)))
-    return fail(kInvalidArgument, "NULL pointer");
+  if (num_points < 0 || points_per_key < 1 || num_points % points_per_key != 0)
+    return fail(kInvalidArgument, "num_points must be a non-negative multiple of points_per_key");
   PointParams p;
-  p.n = num_points;
-  p.points_per_key = points_per_key;
-  p.num_levels = num_levels;
-  p.key_seed = key_seed;
-  p.party = party;
-  p.seeds_in = seeds_in;
-  p.ctrl_in = control_in;
-  p.tree_index = tree_index;
-  p.block_index = block_index;
-  p.cw_seed = cw_seed;
-  p.cw_left = cw_left;
-  p.cw_right = cw_right;
-  p.vcw = value_correction;
-  p.vcw_stride = desc->elements_per_block * desc->num_leaves;
+  int st = make_point_params(num_points / points_per_key, points_per_key, num_levels, key_seed,
+                             party, seeds_in, control_in, tree_index, block_index, cw_seed,
+                             cw_left, cw_right, key_left, key_right, key_value, desc,
+                             value_correction, &p);
+  if (st) return st;
+  if (num_points == 0) return kOk;
+  if (!out) return fail(kInvalidArgument, "NULL pointer");
+  p.num_items = p.num_keys * p.half;
   p.out = (char*)out;
-  p.esz = packed_size(desc);
-  p.rkl = expand_key(key_left);
-  p.rkd = xor_keys(p.rkl, expand_key(key_right));
-  p.rkv = expand_key(key_value);
+  return launch_points<false>(p, desc, value_correction, (hipStream_t)stream);
+}
+
+int dpf_hip_eval_points_batch(int64_t num_keys, int64_t points_per_key, int shared_points,
+                              int num_levels, int cw_stride, int block_index_bits,
+                              const dpf_block* key_seed,
+                              const uint8_t* party, const dpf_block* points,
+                              const dpf_block* cw_seed, const uint8_t* cw_left,
+                              const uint8_t* cw_right, const dpf_aes_key* key_left,
+                              const dpf_aes_key* key_right, const dpf_aes_key* key_value,
+                              const dpf_value_desc* desc, const dpf_block* value_correction,
+                              void* out, void* stream) {
+  if (block_index_bits < 0 || block_index_bits > 7 || num_levels + block_index_bits > 128)
+    return fail(kInvalidArgument, "block_index_bits out of range");
+  PointParams p;
+  int st = make_point_params(num_keys, points_per_key, num_levels, key_seed, party, nullptr,
+                             nullptr, points, nullptr, cw_seed, cw_left, cw_right, key_left,
+                             key_right, key_value, desc, value_correction, &p);
+  if (st) return st;
+  if (!key_seed) return fail(kInvalidArgument, "NULL pointer");
+  if (cw_stride < num_levels) return fail(kInvalidArgument, "cw_stride < num_levels");
+  if (num_keys == 0) return kOk;
+  if (!out) return fail(kInvalidArgument, "NULL pointer");
+  p.cw_stride = cw_stride;
+  p.bib = block_index_bits;
+  p.shared_points = shared_points ? 1 : 0;
+  p.num_items = p.num_keys * p.half;
+  p.out = (char*)out;
+  return launch_points<false>(p, desc, value_correction, (hipStream_t)stream);
+}
+
+int dpf_hip_eval_points_sum(int64_t num_keys, int64_t num_points, int num_levels, int cw_stride,
+                            int block_index_bits, const dpf_block* key_seed, const uint8_t* party,
+                            const dpf_block* points, const dpf_block* cw_seed,
+                            const uint8_t* cw_left, const uint8_t* cw_right,
+                            const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                            const dpf_aes_key* key_value, const dpf_value_desc* desc,
+                            const dpf_block* value_correction, uint64_t* workspace, void* out,
+                            void* stream) {
+  if (num_points == 0 && num_keys >= 0) return kOk;
+  if (block_index_bits < 0 || block_index_bits > 7 || num_levels + block_index_bits > 128)
+    return fail(kInvalidArgument, "block_index_bits out of range");
+  PointParams p;
+  int st = make_point_params(num_keys, num_points, num_levels, key_seed, party, nullptr, nullptr,
+                             points, nullptr, cw_seed, cw_left, cw_right, key_left, key_right,
+                             key_value, desc, value_correction, &p);
+  if (st) return st;
+  if (!key_seed) return fail(kInvalidArgument, "NULL pointer");
+  if (cw_stride < num_levels) return fail(kInvalidArgument, "cw_stride < num_levels");
+  p.cw_stride = cw_stride;
+  p.bib = block_index_bits;
+  if (!out || !workspace) return fail(kInvalidArgument, "NULL pointer");
   hipStream_t s = (hipStream_t)stream;
-  if (fast_int(desc)) {
-    const bool x = desc->kind[0] == DPF_LEAF_XOR;
-    switch (desc->bits[0]) {
-      case 8: return x ? launch_points_fast<8, true>(p, s) : launch_points_fast<8, false>(p, s);
-      case 16: return x ? launch_points_fast<16, true>(p, s) : launch_points_fast<16, false>(p, s);
-      case 32: return x ? launch_points_fast<32, true>(p, s) : launch_points_fast<32, false>(p, s);
-      case 64: return x ? launch_points_fast<64, true>(p, s) : launch_points_fast<64, false>(p, s);
-      default: return x ? launch_points_fast<128, true>(p, s) : launch_points_fast<128, false>(p, s);
-    }
+  const size_t wide_bytes = (size_t)num_points * desc->num_leaves * 3 * sizeof(uint64_t);
+  HIP_TRY(hipMemsetAsync(workspace, 0, wide_bytes, s));
+  if (num_keys > 0) {
+    // Enough (chunk, pair) items to fill every CU's 1024 threads a few times.
+    const int64_t want = (int64_t)num_cus() * kBlock * 4;
+    int64_t chunks = (want + p.half - 1) / p.half;
+    if (chunks > num_keys) chunks = num_keys;
+    p.chunk_keys = (num_keys + chunks - 1) / chunks;
+    chunks = (num_keys + p.chunk_keys - 1) / p.chunk_keys;
+    p.shared_points = 1;
+    p.num_items = chunks * p.half;
+    p.wide = reinterpret_cast<unsigned long long*>(workspace);
+    st = launch_points<true>(p, desc, value_correction, s);
+    if (st) return st;
   }
-  GenericLeaf g;
-  g.d = *desc;
-  g.vcw = value_correction;
-  g.party = 0;
-  g.elements_per_leaf = 1;
-  g.esz = p.esz;
-  hipLaunchKernelGGL((eval_points_kernel<GenericLeaf, 8, false, false>), dim3(grid_for(num_points)),
-                     dim3(kBlock), 0, s, p, g);
+  int64_t g = (num_points + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(finalize_sums_kernel, dim3((unsigned)g), dim3(256), 0, s, num_points, *desc,
+                     reinterpret_cast<const unsigned long long*>(workspace), (char*)out);
   HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_count_out_of_range(int64_t n, const dpf_block* points, int log_domain_size,
+                               int64_t* count, void* stream) {
+  if (!count || n < 0 || log_domain_size < 0 || log_domain_size > 128)
+    return fail(kInvalidArgument, "bad arguments");
+  *count = 0;
+  if (n == 0 || log_domain_size == 128) return kOk;
+  if (!points) return fail(kInvalidArgument, "NULL pointer");
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&d, sizeof(*d), s));
+  HIP_TRY(hipMemsetAsync(d, 0, sizeof(*d), s));
+  int64_t g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(count_out_of_range_kernel, dim3((unsigned)g), dim3(256), 0, s, n, points,
+                     log_domain_size, d);
+  HIP_TRY(hipGetLastError());
+  unsigned long long h = 0;
+  HIP_TRY(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipFreeAsync(d, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  *count = (int64_t)h;
   return kOk;
 }
 

@@ -330,6 +330,59 @@ class DistributedPointFunction:
         n = out.size // size
         return out.reshape(n, size) if packed else _natural(vt, out, n)
 
+    # -- key batches -------------------
+    def make_key_batch(self, keys: Sequence[pb.DpfKey]):
+        """SoA image of `keys` (host); .upload(begin, end, stream) puts rows on the GPU."""
+        return _call(self._impl.make_key_batch, [k.SerializeToString() for k in keys])
+
+    def key_from_batch(self, batch, k: int) -> pb.DpfKey:
+        key = pb.DpfKey()
+        key.ParseFromString(_call(self._impl.key_from_batch, batch, int(k)))
+        return key
+
+    def generate_key_batch(self, alphas: Sequence[int], beta: Sequence,
+                           root_seeds: Optional[np.ndarray] = None, threads: int = 0):
+        """Both parties' key batches for every alpha (shared beta per hierarchy
+        level), generated on `threads` host threads.  root_seeds: uint64 (2n, 2)
+        array ({low, high} per seed, two per key) or None for fresh randomness."""
+        al = alphas if isinstance(alphas, np.ndarray) else u128_array(alphas)
+        return _call(self._impl.generate_key_batch, al, self._betas(beta), root_seeds, int(threads))
+
+    def upload_key_batch(self, batch, begin: int = 0, end: Optional[int] = None, stream=None):
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        end = batch.num_keys if end is None else end
+        return _call(batch.upload, int(begin), int(end), s.cuda_stream)
+
+    def evaluate_at_batch_to_device(self, device_batch, hierarchy_level: int, points,
+                                    points_per_key: int, out, shared_points: bool = False,
+                                    stream=None) -> int:
+        """EvaluateAt for every key of a device batch at device points (a torch
+        int64 tensor (n, 2) of {low, high}); packed outputs [key][point] in `out`."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        return _call(self._impl.evaluate_at_batch_to_device, device_batch, int(hierarchy_level),
+                     points.data_ptr(), int(points_per_key), bool(shared_points), out.data_ptr(),
+                     out.numel() * out.element_size(), s.cuda_stream)
+
+    def evaluate_at_batch_sum_to_device(self, device_batch, hierarchy_level: int, points, out,
+                                        stream=None) -> None:
+        """out[j] = group sum over the batch's keys of EvaluateAt(key, points[j])."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        _call(self._impl.evaluate_at_batch_sum_to_device, device_batch, int(hierarchy_level),
+              points.data_ptr(), int(points.shape[0]), out.data_ptr(), s.cuda_stream)
+
+    def sum_packed_shares(self, hierarchy_level: int, shares: np.ndarray, num_shares: int,
+                          count: int) -> np.ndarray:
+        """Group sum of num_shares packed vectors of `count` elements (host)."""
+        return _call(self._impl.sum_packed_shares, int(hierarchy_level),
+                     np.ascontiguousarray(shares, dtype=np.uint8).reshape(-1), int(num_shares),
+                     int(count))
+
+    def packed_size(self, h: int) -> int:
+        return self._impl.packed_size(h)
+
     def tree_levels_needed(self) -> int:
         return self._impl.tree_levels_needed()
 

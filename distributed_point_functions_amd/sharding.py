@@ -51,3 +51,42 @@ def max_over_ranks(value: float, device=None) -> float:
                      device=device if device is not None else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ---------------------------------------------------------------------------
+# Key-batch sharding (configs 4 and 5, SURVEY.md section 8e)
+# ---------------------------------------------------------------------------
+# Batched EvaluateAt and heavy-hitters aggregation over K keys split the keys
+# into `world` contiguous row ranges (DeviceKeyBatch.upload(begin, end)).
+# Per-key outputs stay on their rank; the aggregation variant reduces over the
+# rank's keys on the device (dpf_hip_eval_points_sum) and then combines the
+# per-rank partial sums -- the only data-path exchange: one all_gather of
+# num_points packed elements (a few KiB over xGMI) followed by the group sum
+# (integers mod 2^bits, IntModN mod N, XOR) on every rank.  All-gather rather
+# than all_reduce(SUM) because the group is not always the integers mod 2^64.
+
+def key_range(num_keys: int, world: int, rank: int) -> tuple:
+    """[begin, end) of the keys rank `rank` owns (balanced contiguous split)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad world/rank")
+    return num_keys * rank // world, num_keys * (rank + 1) // world
+
+
+def all_gather_shares(packed):
+    """All-gathers one rank's packed partial sums (a uint8 torch tensor, CPU for
+    gloo or CUDA for RCCL) and returns the stacked [world, bytes] host array."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return packed.cpu().numpy().reshape(1, -1)
+    parts = [torch.empty_like(packed) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, packed.contiguous())
+    return np.stack([p.cpu().numpy().reshape(-1) for p in parts])
+
+
+def aggregate_shares(dpf, hierarchy_level: int, packed, count: int):
+    """Group sum over ranks of `count`-element packed partial sums: the
+    cross-GPU step of the aggregation variant."""
+    stacked = all_gather_shares(packed)
+    return dpf.sum_packed_shares(hierarchy_level, stacked, stacked.shape[0], count)

@@ -37,6 +37,7 @@
 #include "dpf/distributed_point_function.pb.h"
 #include "dpf/internal/proto_validator.h"
 #include "dpf/internal/value_type_helpers.h"
+#include "dpf/key_batch.h"
 #include "dpf/span.h"
 #include "dpf/status.h"
 #include "dpf/uint128.h"
@@ -213,6 +214,40 @@ class DistributedPointFunction {
                                                        Span<const uint128> points,
                                                        int64_t points_per_key) const;
 
+  // ---- key batches ------------------
+  // SoA image of `keys` (each validated like CreateEvaluationContext does).
+  StatusOr<KeyBatch> MakeKeyBatch(Span<const DpfKey* const> keys) const;
+  // Row k of `batch` as a DpfKey proto (inverse of MakeKeyBatch).
+  StatusOr<DpfKey> KeyFromBatch(const KeyBatch& batch, int64_t k) const;
+  // Key generation for many alphas at once, straight into SoA form, on
+  // `num_threads` host threads (0 = hardware concurrency).  Key k of the pair
+  // is what GenerateKeysIncrementalWithSeeds(alphas[k], beta, root_seeds[2k],
+  // root_seeds[2k+1]) returns; with empty root_seeds they are drawn like
+  // GenerateKeysIncremental draws them.  `beta` is shared by all keys.
+  StatusOr<std::pair<KeyBatch, KeyBatch>> GenerateKeyBatch(Span<const uint128> alphas,
+                                                           Span<const Value> beta,
+                                                           Span<const uint128> root_seeds,
+                                                           int num_threads = 0) const;
+  // EvaluateAt(key_k, hierarchy_level, points_k) for every key of a device
+  // batch.  `device_points` are raw domain points (uint128 memory images) in
+  // device memory: points_per_key per key ([key][point]), or one shared set of
+  // points_per_key points when `shared_points`.  Writes num_keys *
+  // points_per_key packed elements ([key][point]) to device_out.
+  StatusOr<int64_t> EvaluateAtBatchToDevice(const DeviceKeyBatch& keys, int hierarchy_level,
+                                            const void* device_points, int64_t points_per_key,
+                                            bool shared_points, void* device_out,
+                                            int64_t capacity_bytes, void* stream) const;
+  // Aggregation variant: out[j] = sum over the batch's keys of
+  // EvaluateAt(key_k, hierarchy_level, point_j), in the value type's group,
+  // for one shared set of num_points device points (num_points packed elements).
+  Status EvaluateAtBatchSumToDevice(const DeviceKeyBatch& keys, int hierarchy_level,
+                                    const void* device_points, int64_t num_points,
+                                    void* device_out, void* stream) const;
+  // Group sum of `num_shares` packed output vectors of `count` elements each
+  // (host memory), e.g. per-GPU partial sums after an all-gather.
+  StatusOr<std::vector<uint8_t>> SumPackedShares(int hierarchy_level, const uint8_t* shares,
+                                                 int64_t num_shares, int64_t count) const;
+
   // Introspection.
   int tree_levels_needed() const { return validator_->tree_levels_needed(); }
   const std::vector<int>& hierarchy_to_tree() const { return validator_->hierarchy_to_tree(); }
@@ -241,6 +276,13 @@ class DistributedPointFunction {
   }
 
   // Key generation pieces (cc:63-204).
+  StatusOr<std::vector<uint128>> ComputeValueCorrectionLeaves(int hierarchy_level,
+                                                              const uint128 seeds[2], uint128 alpha,
+                                                              Span<const uint128> beta_leaves,
+                                                              bool invert) const;
+  Status CheckValueCorrectionKnown(int hierarchy_level) const;
+  Status GenerateNextCore(int tree_level, uint128 alpha, uint128 seeds[2], bool control_bits[2],
+                          uint128* seed_correction, bool ccw[2]) const;
   StatusOr<std::vector<Value>> ComputeValueCorrection(int hierarchy_level, const uint128 seeds[2],
                                                       uint128 alpha, const Value& beta,
                                                       bool invert) const;

@@ -146,6 +146,50 @@ int dpf_hip_eval_points(int64_t num_points, int64_t points_per_key, int num_leve
                         const dpf_value_desc* desc, const dpf_block* value_correction,
                         void* out, void* stream);
 
+/* ---- a11 + SURVEY 8e: batched point evaluation over a key batch ------------
+ * Config 4 (2^20 keys x 2^10 points).  Key k < num_keys is the SoA row k of a
+ * key batch: root key_seed[k], party[k], correction words cw_seed[k*cw_stride
+ * + j], cw_left[...], cw_right[...] (j < num_levels = the hierarchy level's
+ * tree depth <= cw_stride, the key's correction-word count) and value
+ * corrections value_correction[k*E*num_leaves ...].
+ * `points` are raw domain points (dpf_block = uint128): the tree path is
+ * point >> block_index_bits and the element index point & (2^bits - 1)
+ * (distributed_point_function.cc:206-221).  Point j of key k is
+ * points[shared_points ? j : k*points_per_key + j]; the output element
+ * k*points_per_key + j (packed) equals EvaluateAt(key_k, {point}).
+ * When points_per_key is even and (points_per_key / 2) % 64 == 0 every
+ * wavefront works on one key (scalar correction-word loads). */
+int dpf_hip_eval_points_batch(int64_t num_keys, int64_t points_per_key, int shared_points,
+                              int num_levels, int cw_stride, int block_index_bits,
+                              const dpf_block* key_seed,
+                              const uint8_t* party, const dpf_block* points,
+                              const dpf_block* cw_seed, const uint8_t* cw_left,
+                              const uint8_t* cw_right, const dpf_aes_key* key_left,
+                              const dpf_aes_key* key_right, const dpf_aes_key* key_value,
+                              const dpf_value_desc* desc, const dpf_block* value_correction,
+                              void* out, void* stream);
+
+/* Aggregation variant: every key is evaluated at the SAME num_points points
+ * and   out[j] = sum over k < num_keys of EvaluateAt(key_k, points[j])
+ * is written packed, the sum taken in the value type's group (integers mod
+ * 2^bits, IntModN mod N, XorWrapper by XOR; tuples element-wise).
+ * `workspace` (device) holds num_points * desc->num_leaves * 3 uint64 (192-bit
+ * exact per-leaf sums) and is cleared by the call. */
+int dpf_hip_eval_points_sum(int64_t num_keys, int64_t num_points, int num_levels, int cw_stride,
+                            int block_index_bits, const dpf_block* key_seed, const uint8_t* party,
+                            const dpf_block* points, const dpf_block* cw_seed,
+                            const uint8_t* cw_left, const uint8_t* cw_right,
+                            const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                            const dpf_aes_key* key_value, const dpf_value_desc* desc,
+                            const dpf_block* value_correction, uint64_t* workspace, void* out,
+                            void* stream);
+
+/* Number of points[i] >= 2^log_domain_size (the EvaluateAt range check,
+ * distributed_point_function.h:861-874, for device-resident points).
+ * Synchronous: *count is a host int64. */
+int dpf_hip_count_out_of_range(int64_t n, const dpf_block* points, int log_domain_size,
+                               int64_t* count, void* stream);
+
 /* ---- gather for EvaluateUntil with prefixes (h:822-835) -------------------
  * out[i*count + j] = in[src_offset[i] + j], elements of elem_size bytes. */
 int dpf_hip_gather(int64_t num_rows, int64_t count, int elem_size, const int64_t* src_offset,

@@ -67,6 +67,13 @@ def main(tag, match="expand_kernel", aes_per_launch=None, leaves_per_launch=None
 
 
 if __name__ == "__main__":
-    tag = sys.argv[1]
-    D = 29
-    main(tag, aes_per_launch=2 * (2**D - 1) + 2**D, leaves_per_launch=2**30)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--match", default="expand_kernel", help="substring of the kernel name")
+    ap.add_argument("--aes", type=int, default=2 * (2**29 - 1) + 2**29,
+                    help="algorithmic AES blocks per launch (default: config 2, D = 29)")
+    ap.add_argument("--leaves", type=int, default=2**30,
+                    help="output elements per launch (8 B each for the write figure)")
+    a = ap.parse_args()
+    main(a.tag, match=a.match, aes_per_launch=a.aes, leaves_per_launch=a.leaves)

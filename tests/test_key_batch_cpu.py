@@ -1,0 +1,156 @@
+"""Key batches on the host (no GPU): SoA ingestion of DpfKeys, batched
+multi-threaded key generation and the host-side share sum.  Row k of a
+generated batch must be exactly the DpfKey the single-key keygen
+(GenerateKeysIncrementalWithSeeds, distributed_point_function.cc:619-687)
+produces for the same alpha and root seeds, which test_host_api_cpu pins to
+the oracle."""
+import numpy as np
+import pytest
+
+import oracle as O
+import ref_grids as G
+from distributed_point_functions_amd import dpf as D
+from test_host_api_cpu import params, vt_from_oracle, leaves_value
+
+MASK64 = (1 << 64) - 1
+
+GRID = [
+    [(128, ("int", 64), 0)],
+    [(20, ("int", 8), 0)],
+    [(16, ("xor", 128), 0)],
+    [(5, ("int", 16), 0), (12, ("int", 64), 0), (40, ("int", 128), 0)],
+    [(8, ("tuple", [("intmodn", 32, 4294967291)] * 2), 64.0),
+     (16, ("tuple", [("intmodn", 32, 4294967291)] * 2), 64.0)],
+    [(12, ("tuple", [("int", 32), ("intmodn", 64, G.M64)]), 48.0)],
+]
+
+
+def make(levels):
+    dpf = D.DistributedPointFunction.create_incremental(params(levels))
+    for _, vt, _ in levels:
+        dpf.register_value_type(vt_from_oracle(vt))
+    return dpf
+
+
+def seeds_array(rng, n):
+    return rng.integers(0, 1 << 63, size=(2 * n, 2), dtype=np.uint64)
+
+
+def betas_for(levels, k=0):
+    return [leaves_value(vt, [(k + 7 * h + 1) % 251 + 1] * len(O.leaves(vt)))
+            for h, (_, vt, _) in enumerate(levels)]
+
+
+@pytest.mark.parametrize("levels", GRID, ids=str)
+def test_generate_key_batch_rows_equal_single_keygen(levels):
+    dpf = make(levels)
+    rng = np.random.default_rng(len(levels) * 7 + levels[-1][0])
+    n = 37
+    top = levels[-1][0]
+    alphas = [int(rng.integers(0, 1 << 62)) % (1 << top) if top < 128 else
+              (int(rng.integers(0, 1 << 62)) << 66) | int(rng.integers(0, 1 << 62)) for _ in range(n)]
+    seeds = seeds_array(rng, n)
+    beta = betas_for(levels)
+    b0, b1 = dpf.generate_key_batch(alphas, beta, root_seeds=seeds, threads=3)
+    assert b0.num_keys == n and b1.num_keys == n
+    assert b0.num_levels == dpf.tree_levels_needed() - 1
+    np.testing.assert_array_equal(b0.party(), np.zeros(n, np.uint8))
+    np.testing.assert_array_equal(b1.party(), np.ones(n, np.uint8))
+    for k in range(n):
+        s0 = int(seeds[2 * k, 0]) | int(seeds[2 * k, 1]) << 64
+        s1 = int(seeds[2 * k + 1, 0]) | int(seeds[2 * k + 1, 1]) << 64
+        k0, k1 = dpf.generate_keys_incremental(alphas[k], beta, seeds=(s0, s1))
+        assert dpf.key_from_batch(b0, k).SerializeToString() == k0.SerializeToString()
+        assert dpf.key_from_batch(b1, k).SerializeToString() == k1.SerializeToString()
+
+
+def test_generate_key_batch_thread_count_invariant():
+    levels = GRID[3]
+    dpf = make(levels)
+    rng = np.random.default_rng(3)
+    n = 1000
+    alphas = [int(x) for x in rng.integers(0, 1 << 40, size=n)]
+    seeds = seeds_array(rng, n)
+    beta = betas_for(levels)
+    ref = dpf.generate_key_batch(alphas, beta, root_seeds=seeds, threads=1)
+    for t in (2, 7, 0):
+        got = dpf.generate_key_batch(alphas, beta, root_seeds=seeds, threads=t)
+        for a, b in zip(ref, got):
+            np.testing.assert_array_equal(a.seeds(), b.seeds())
+            for k in (0, 499, 999):
+                assert (dpf.key_from_batch(a, k).SerializeToString() ==
+                        dpf.key_from_batch(b, k).SerializeToString())
+
+
+def test_generate_key_batch_random_seeds_differ():
+    dpf = make(GRID[1])
+    b0, b1 = dpf.generate_key_batch([1, 1], betas_for(GRID[1]))
+    s = np.concatenate([b0.seeds(), b1.seeds()])
+    assert len({tuple(r) for r in s.tolist()}) == 4
+
+
+@pytest.mark.parametrize("levels", GRID, ids=str)
+def test_make_key_batch_roundtrip(levels):
+    dpf = make(levels)
+    keys = []
+    for k in range(5):
+        a, b = dpf.generate_keys_incremental(k * 3 + 1, betas_for(levels, k), seeds=(10 + k, 20 + k))
+        keys += [a, b]
+    batch = dpf.make_key_batch(keys)
+    assert batch.num_keys == len(keys)
+    for k, key in enumerate(keys):
+        assert dpf.key_from_batch(batch, k).SerializeToString() == key.SerializeToString()
+
+
+def test_key_batch_errors():
+    levels = GRID[1]
+    dpf = make(levels)
+    beta = betas_for(levels)
+    with pytest.raises(D.DpfStatusError) as e:
+        dpf.generate_key_batch([1 << 20], beta)
+    assert e.value.message == "`alpha` must be smaller than the output domain size"
+    with pytest.raises(D.DpfStatusError) as e:
+        dpf.generate_key_batch([1, 2], beta, root_seeds=np.zeros((3, 2), np.uint64))
+    assert e.value.code_name == "INVALID_ARGUMENT"
+    with pytest.raises(D.DpfStatusError) as e:
+        dpf.generate_key_batch([1], beta + beta)
+    assert e.value.message == "`beta` has to have the same size as `parameters` passed at construction"
+    batch, _ = dpf.generate_key_batch([1, 2], beta)
+    with pytest.raises(D.DpfStatusError):
+        dpf.key_from_batch(batch, 2)
+    other = make(GRID[0])
+    with pytest.raises(D.DpfStatusError) as e:
+        other.key_from_batch(batch, 0)
+    assert e.value.message == "key batch does not match this DistributedPointFunction"
+    bad = dpf.generate_keys_incremental(1, beta)[0]
+    del bad.correction_words[-1]
+    with pytest.raises(D.DpfStatusError):
+        dpf.make_key_batch([bad])
+
+
+@pytest.mark.parametrize("vt", [("int", 64), ("int", 8), ("xor", 128),
+                                ("tuple", [("intmodn", 32, 4294967291)] * 2),
+                                ("tuple", [("int", 16), ("intmodn", 128, G.M80)])], ids=str)
+def test_sum_packed_shares_matches_oracle_group_sum(vt):
+    levels = [(10, vt, 48.0)]
+    dpf = make(levels)
+    rng = np.random.default_rng(11)
+    size = O.packed_size(vt)
+    num_shares, count = 5, 33
+    # Valid group elements: reduce IntModN leaves below their modulus.
+    vals = []
+    for _ in range(num_shares * count):
+        leaves = []
+        for kind, bits, mod in O.leaves(vt):
+            x = int(rng.integers(0, 1 << 62)) << 66 | int(rng.integers(0, 1 << 62))
+            x &= (1 << bits) - 1
+            if kind == "intmodn":
+                x %= mod
+            leaves.append(x)
+        vals.append(O.pack_element(vt, leaves))
+    shares = np.frombuffer(b"".join(vals), np.uint8).reshape(num_shares, count, size)
+    got = dpf.sum_packed_shares(0, shares, num_shares, count).reshape(count, size)
+    want = shares[0]
+    for r in range(1, num_shares):
+        want = O.add_packed(vt, want, shares[r])
+    np.testing.assert_array_equal(got, want)

@@ -1,0 +1,175 @@
+"""Batched EvaluateAt over a device key batch (SURVEY.md config 4 and its
+aggregation variant) on an MI355X, bit-exact against the CPU oracle's
+EvaluateAtImpl (distributed_point_function.h:839-1010) run key by key on the
+same keys (oracle keygen with the same root seeds)."""
+import numpy as np
+import pytest
+
+import oracle as O
+import ref_grids as G
+from distributed_point_functions_amd import dpf as D
+from test_host_api_cpu import vt_from_oracle, leaves_value
+from test_key_batch_cpu import make
+
+pytestmark = pytest.mark.gpu
+MASK64 = (1 << 64) - 1
+
+
+def _rand_u128(rng, n, log):
+    out = []
+    for _ in range(n):
+        x = (int(rng.integers(0, 1 << 63)) << 65) ^ int(rng.integers(0, 1 << 63)) ^ int(rng.integers(0, 4))
+        out.append(x & ((1 << log) - 1) if log < 128 else x & ((1 << 128) - 1))
+    return out
+
+
+def _dev_points(pts):
+    import torch
+    return torch.from_numpy(D.u128_array(pts).view(np.int64)).cuda()
+
+
+def _setup(levels, n_keys, seed, party_mix=True):
+    dpf = make(levels)
+    P = O.OracleParams(levels)
+    rng = np.random.default_rng(seed)
+    top = levels[-1][0]
+    alphas = _rand_u128(rng, n_keys, top)
+    seeds = rng.integers(1, 1 << 62, size=(2 * n_keys, 2), dtype=np.uint64)
+    beta_leaves = [[(7 * h + 3) % 200 + 1] * len(O.leaves(vt)) for h, (_, vt, _) in enumerate(levels)]
+    beta = [leaves_value(vt, b) for (_, vt, _), b in zip(levels, beta_leaves)]
+    b0, b1 = dpf.generate_key_batch(alphas, beta, root_seeds=seeds, threads=4)
+    okeys = []
+    for k in range(n_keys):
+        s0 = int(seeds[2 * k, 0]) | int(seeds[2 * k, 1]) << 64
+        s1 = int(seeds[2 * k + 1, 0]) | int(seeds[2 * k + 1, 1]) << 64
+        okeys.append(O.generate_keys(P, alphas[k], beta_leaves, s0, s1))
+    # Mixed-party batch: even keys party 0, odd keys party 1.
+    keys = [dpf.key_from_batch(b0 if (k % 2 == 0 or not party_mix) else b1, k) for k in range(n_keys)]
+    mixed = dpf.make_key_batch(keys)
+    oks = [okeys[k][0 if (k % 2 == 0 or not party_mix) else 1] for k in range(n_keys)]
+    return dpf, P, rng, mixed, oks, alphas, okeys, (b0, b1)
+
+
+CASES = [
+    # (levels, hierarchy level, keys, points per key)
+    ([(128, ("int", 64), 0)], 0, 6, 256),      # uniform-key waves (128 points per half)
+    ([(128, ("int", 64), 0)], 0, 5, 7),        # odd points per key, ragged pairs
+    ([(40, ("int", 128), 0)], 0, 9, 130),
+    ([(30, ("int", 8), 0)], 0, 4, 200),        # 16 elements per block
+    ([(64, ("xor", 128), 0)], 0, 3, 64),
+    ([(20, ("xor", 16), 0)], 0, 3, 129),
+    ([(24, ("tuple", [("intmodn", 32, G.M32)] * 2), 64.0)], 0, 5, 128),
+    ([(10, ("int", 16), 0), (50, ("int", 64), 0)], 0, 4, 100),
+    ([(10, ("int", 16), 0), (50, ("int", 64), 0)], 1, 4, 100),
+    ([(12, ("tuple", [("int", 32), ("intmodn", 64, G.M64)]), 48.0)], 0, 3, 1),
+]
+
+
+@pytest.mark.parametrize("levels,h,n_keys,ppk", CASES, ids=str)
+def test_evaluate_at_batch_per_key_points(levels, h, n_keys, ppk):
+    import torch
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=n_keys * 31 + ppk)
+    log = levels[h][0]
+    pts = _rand_u128(rng, n_keys * ppk, log)
+    dev_batch = dpf.upload_key_batch(batch)
+    size = dpf.packed_size(h)
+    out = torch.empty(n_keys * ppk * size, dtype=torch.uint8, device="cuda")
+    n = dpf.evaluate_at_batch_to_device(dev_batch, h, _dev_points(pts), ppk, out)
+    torch.cuda.synchronize()
+    assert n == n_keys * ppk
+    got = out.cpu().numpy().reshape(n_keys * ppk, size)
+    for k in range(n_keys):
+        want = O.evaluate_at(P, oks[k], h, pts[k * ppk:(k + 1) * ppk])
+        np.testing.assert_array_equal(got[k * ppk:(k + 1) * ppk], want, err_msg=f"key {k}")
+
+
+@pytest.mark.parametrize("levels,h,n_keys,ppk", CASES[:4] + CASES[6:7], ids=str)
+def test_evaluate_at_batch_shared_points(levels, h, n_keys, ppk):
+    import torch
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=ppk)
+    pts = _rand_u128(rng, ppk, levels[h][0])
+    dev_batch = dpf.upload_key_batch(batch)
+    size = dpf.packed_size(h)
+    out = torch.empty(n_keys * ppk * size, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_to_device(dev_batch, h, _dev_points(pts), ppk, out, shared_points=True)
+    got = out.cpu().numpy().reshape(n_keys, ppk, size)
+    for k in range(n_keys):
+        np.testing.assert_array_equal(got[k], O.evaluate_at(P, oks[k], h, pts))
+
+
+SUM_CASES = [
+    ([(128, ("int", 64), 0)], 0, 64, 256),
+    ([(128, ("int", 64), 0)], 0, 7, 5),
+    ([(40, ("int", 128), 0)], 0, 33, 130),
+    ([(30, ("int", 8), 0)], 0, 20, 64),
+    ([(64, ("xor", 128), 0)], 0, 9, 128),
+    ([(24, ("tuple", [("intmodn", 32, G.M32)] * 2), 64.0)], 0, 17, 128),
+    ([(12, ("tuple", [("int", 16), ("intmodn", 128, G.M80)]), 48.0)], 0, 6, 10),
+    ([(20, ("intmodn", 64, G.M64), 48.0)], 0, 40, 20),
+]
+
+
+@pytest.mark.parametrize("levels,h,n_keys,npts", SUM_CASES, ids=str)
+def test_evaluate_at_batch_sum(levels, h, n_keys, npts):
+    import torch
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=n_keys + npts)
+    vt = levels[h][1]
+    pts = _rand_u128(rng, npts, levels[h][0])
+    dev_batch = dpf.upload_key_batch(batch)
+    size = dpf.packed_size(h)
+    out = torch.empty(npts * size, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_sum_to_device(dev_batch, h, _dev_points(pts), out)
+    got = out.cpu().numpy().reshape(npts, size)
+    want = O.evaluate_at(P, oks[0], h, pts)
+    for k in range(1, n_keys):
+        want = O.add_packed(vt, want, O.evaluate_at(P, oks[k], h, pts))
+    np.testing.assert_array_equal(got, want)
+
+
+def test_two_server_reconstruction_through_batch_sums():
+    """Heavy-hitters style aggregation: the two servers' batch sums add up to
+    the number of clients whose alpha equals each point (beta = 1)."""
+    import torch
+    levels = [(32, ("int", 64), 0)]
+    dpf = make(levels)
+    rng = np.random.default_rng(9)
+    n = 512
+    hot = [5, 77, 1 << 31]
+    alphas = [hot[i % 3] if i % 4 else int(rng.integers(0, 1 << 32)) for i in range(n)]
+    b0, b1 = dpf.generate_key_batch(alphas, [D.to_value(D.integer_type(64), 1)], threads=4)
+    pts = hot + [6, 0, (1 << 32) - 1]
+    sums = []
+    for b in (b0, b1):
+        out = torch.empty(len(pts) * 8, dtype=torch.uint8, device="cuda")
+        dpf.evaluate_at_batch_sum_to_device(dpf.upload_key_batch(b), 0, _dev_points(pts), out)
+        sums.append(out.cpu().numpy().view(np.uint64))
+    total = (sums[0] + sums[1]).tolist()
+    want = [sum(1 for a in alphas if a == p) for p in pts]
+    assert total == want
+
+
+def test_batch_range_upload_and_errors():
+    import torch
+    levels = [(20, ("int", 32), 0)]
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, 10, seed=1)
+    pts = _rand_u128(rng, 8, 20)
+    part = dpf.upload_key_batch(batch, 3, 7)
+    assert (part.num_keys, part.first_key) == (4, 3)
+    out = torch.empty(4 * 8 * 4, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_to_device(part, 0, _dev_points(pts), 8, out, shared_points=True)
+    got = out.cpu().numpy().reshape(4, 8, 4)
+    for i in range(4):
+        np.testing.assert_array_equal(got[i], O.evaluate_at(P, oks[3 + i], 0, pts))
+    with pytest.raises(D.DpfStatusError) as e:
+        dpf.evaluate_at_batch_to_device(part, 0, _dev_points([1 << 20]), 1, out, shared_points=True)
+    assert e.value.code_name == "INVALID_ARGUMENT"
+    with pytest.raises(D.DpfStatusError):
+        dpf.evaluate_at_batch_to_device(part, 1, _dev_points(pts), 8, out)
+    small = torch.empty(3, dtype=torch.uint8, device="cuda")
+    with pytest.raises(D.DpfStatusError) as e:
+        dpf.evaluate_at_batch_to_device(part, 0, _dev_points(pts), 8, small)
+    assert e.value.message == "device output buffer too small"
+    other = make([(21, ("int", 32), 0)])
+    with pytest.raises(D.DpfStatusError) as e:
+        other.evaluate_at_batch_to_device(part, 0, _dev_points(pts), 8, out)
+    assert e.value.message == "key batch does not match this DistributedPointFunction"

@@ -97,3 +97,69 @@ def test_partition_helpers():
     with pytest.raises(ValueError):
         S.shard_range(16, 4, 4)
     assert S.max_over_ranks(3.0) == 3.0
+
+
+# ------------------------------------------------- key-batch sharding (config 4/5)
+def _key_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from distributed_point_functions_amd import dpf as D
+    from test_host_api_cpu import params, vt_from_oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        vt = ("tuple", [("intmodn", 32, 4294967291)] * 2)
+        levels = [(16, vt, 64.0)]
+        P = O.OracleParams(levels)
+        dpf = D.DistributedPointFunction.create_incremental(params(levels))
+        dpf.register_value_type(vt_from_oracle(vt))
+        n_keys, pts = 23, [0, 5, 77, 4095, 65535, 1234]
+        rng = np.random.default_rng(17)          # same keys on every rank
+        alphas = [int(a) for a in rng.integers(0, 1 << 16, size=n_keys)]
+        keys = [O.generate_keys(P, a, [[1, 1]], 1000 + k, 2000 + k)[k % 2]
+                for k, a in enumerate(alphas)]
+        lo, hi = S.key_range(n_keys, world, rank)
+        part = None
+        for k in range(lo, hi):
+            v = O.evaluate_at(P, keys[k], 0, pts)
+            part = v if part is None else O.add_packed(vt, part, v)
+        if part is None:
+            part = np.zeros((len(pts), O.packed_size(vt)), np.uint8)
+        total = S.aggregate_shares(dpf, 0, torch.from_numpy(part.reshape(-1).copy()), len(pts))
+        if rank == 0:
+            q.put(total)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_key_batch_shards_aggregate_to_full_sum(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_key_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    total = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    vt = ("tuple", [("intmodn", 32, 4294967291)] * 2)
+    P = O.OracleParams([(16, vt, 64.0)])
+    rng = np.random.default_rng(17)
+    alphas = [int(a) for a in rng.integers(0, 1 << 16, size=23)]
+    pts = [0, 5, 77, 4095, 65535, 1234]
+    want = None
+    for k, a in enumerate(alphas):
+        v = O.evaluate_at(P, O.generate_keys(P, a, [[1, 1]], 1000 + k, 2000 + k)[k % 2], 0, pts)
+        want = v if want is None else O.add_packed(vt, want, v)
+    np.testing.assert_array_equal(total.reshape(want.shape), want)
+
+
+def test_key_range_partition():
+    for n in (0, 1, 7, 1 << 20):
+        for w in (1, 2, 3, 8):
+            rs = [S.key_range(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
