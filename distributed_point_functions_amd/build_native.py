@@ -29,6 +29,10 @@ HIPCC = os.path.join(ROCM, "bin", "hipcc")
 HIP_FLAGS = [
     "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
     "-mcode-object-version=5", "-Wall", "-Wno-unused-function",
+    # The AES rounds are LDS-latency bound: this scheduler keeps ~8-14 table
+    # reads in flight per wave instead of 2-3 (tools/variant_bench.py, r04:
+    # batched points 76 -> 89 G AES/s, expand 82 -> 84).
+    "-mllvm", "-amdgpu-sched-strategy=iterative-ilp",
 ]
 
 

@@ -455,7 +455,7 @@ struct GenericLeaf {
 // Kernels
 // ------------------------------------------------------------------------
 
-__global__ __launch_bounds__(kBlock) void hash_kernel(int64_t n, const dpf_block* __restrict__ in,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void hash_kernel(int64_t n, const dpf_block* __restrict__ in,
                                                       dpf_block* __restrict__ out,
                                                       RoundKeys rk) {
   __shared__ LdsImage lds;
@@ -487,7 +487,7 @@ __device__ __forceinline__ uint32_t path_bit(Block4 p, int pos) {
   return (w >> (pos & 31)) & 1u;
 }
 
-__global__ __launch_bounds__(kBlock) void eval_paths_kernel(PathParams p) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void eval_paths_kernel(PathParams p) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
@@ -522,7 +522,7 @@ struct ExpandParams {
 };
 
 template <class Leaf>
-__global__ __launch_bounds__(kBlock) void expand_kernel(ExpandParams p, Leaf leaf) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void expand_kernel(ExpandParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   leaf.init();
   fill_tables(lds.tab);
@@ -729,7 +729,7 @@ __device__ __forceinline__ u128 leaf_group_add(const dpf_value_desc& d, int k, u
 }
 
 template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM>
-__global__ __launch_bounds__(kBlock) void eval_points_kernel(PointParams p, Leaf leaf) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void eval_points_kernel(PointParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();

@@ -18,7 +18,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdpf_hip.so")
+LIB_PATH = os.environ.get("DPF_HIP_LIB") or os.path.join(_HERE, "lib", "libdpf_hip.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "dpf_hip.h")
 MAX_LEAVES = 16
 LEAF_INT, LEAF_INTMODN, LEAF_XOR = 0, 1, 2
