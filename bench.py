@@ -57,11 +57,15 @@ def parse():
     ap.add_argument("--cpu-chunks", type=int, default=32,
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
     ap.add_argument("--workload", default="full_domain",
-                    choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum"],
+                    choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum",
+                             "synthetic_hierarchical", "synthetic_direct"],
                     help="full_domain = BASELINE configs[1] (the headline); full_domain_u128 = "
                          "configs[2] (2^31 uint128 outputs per GPU, 2^34 over 8 GPUs); "
                          "evaluate_at(_sum) = configs[3] (2^20 keys x 2^10 points, log 128)")
     ap.add_argument("--keys-log", type=int, default=20, help="evaluate_at: log2 keys (all ranks)")
+    ap.add_argument("--domain", type=int, default=32, help="synthetic_*: log2 domain (32 or 128)")
+    ap.add_argument("--distribution", default="uniform", choices=["0.1", "0.5", "uniform"],
+                    help="synthetic_*: 90%% of nonzeros in the first 10%%/50%% of the domain, or uniform")
     ap.add_argument("--points-log", type=int, default=10, help="evaluate_at: log2 points per key")
     return ap.parse_args()
 
@@ -136,6 +140,8 @@ def main():
     args = parse()
     if args.workload.startswith("evaluate_at"):
         return main_evaluate_at(args)
+    if args.workload.startswith("synthetic"):
+        return main_synthetic(args)
     if args.workload == "full_domain_u128" and args.log_domain == LOG_PER_GPU:
         args.log_domain = 31
     import torch
@@ -437,6 +443,61 @@ def main_evaluate_at(args):
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# experiments/README.md (1 key, 2^20 nonzeros, uint32, one Xeon thread @ 2.30 GHz):
+# seconds per iteration by (mode, domain, distribution).
+PUBLISHED_SYNTHETIC = {
+    ("hierarchical", 32): {"0.1": 1.36, "0.5": 2.22, "uniform": 3.31},
+    ("direct", 32): {"0.1": 0.67, "0.5": 0.68, "uniform": 0.70},
+    ("hierarchical", 128): {"0.1": 32.68, "0.5": 35.07, "uniform": 35.95},
+    ("direct", 128): {"0.1": 3.08, "0.5": 3.13, "uniform": 3.13},
+}
+
+
+def main_synthetic(args):
+    """the reference's own published benchmark
+    (experiments/synthetic_data_benchmarks.cc) -- one key, 2^20 nonzeros,
+    uint32, hierarchical EvaluateUntil over levels chosen so no level expands to
+    more than 4 x 2^20 outputs, or direct EvaluateAt at the nonzeros -- run
+    through the same driver restated in C++ on the GPU-backed API.  The
+    reference's CSV inputs are git-LFS stubs; the nonzeros are regenerated
+    with the README's distributions (seeded).  Single key => one GPU."""
+    from distributed_point_functions_amd import dpf as D
+    from distributed_point_functions_amd import hip_abi as H
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("synthetic_* workloads evaluate one key on one GPU")
+    H.load(require_gpu=True)
+    mode = "direct" if args.workload == "synthetic_direct" else "hierarchical"
+    conc = 0.0 if args.distribution == "uniform" else float(args.distribution)
+    host = D.host()
+    # warmup iteration(s) are part of the driver's first call; time a second call.
+    for _ in range(max(args.warmup, 0)):
+        D._call(host.run_synthetic_data_benchmark, args.domain, 1 << 20, conc, 1, 4, 1,
+                mode == "direct", False)
+    r = D._call(host.run_synthetic_data_benchmark, args.domain, 1 << 20, conc, 1, 4,
+                args.steps, mode == "direct", True)
+    pub = PUBLISHED_SYNTHETIC.get((mode, args.domain), {}).get(args.distribution)
+    secs = r["seconds_per_iteration"]
+    outs = sum(r["outputs_per_level"])
+    res = {
+        "metric": f"synthetic_data_benchmarks {mode} evaluation, domain 2^{args.domain}, "
+                  f"distribution {args.distribution}: seconds per iteration (1 key, 2^20 nonzeros, uint32)",
+        "value": secs, "unit": "s/iteration", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": secs * 1e3, "higher_is_better": False,
+        "scaling": "none", "vs_baseline": (secs / pub) if pub else None,
+        "published_reference_s": pub, "dtype": "u32",
+        "data": "synthetic: 2^20 distinct nonzeros regenerated with the README's distributions "
+                "(the reference CSVs are git-LFS stubs); seed 1",
+        "config": {"workload": f"{mode} evaluation of one DpfKey through the DistributedPointFunction "
+                               f"API (EvaluateUntil per level / EvaluateAt), domain 2^{args.domain}",
+                   "levels_to_evaluate": r["levels_to_evaluate"],
+                   "prefixes_per_level": r["prefixes_per_level"],
+                   "outputs_per_level": r["outputs_per_level"],
+                   "key_size_bytes": r["key_size_bytes"]},
+        "outputs_per_s": outs / secs, "verified_two_server_reconstruction": r["verified"],
+    }
+    print(json.dumps(res), flush=True)
 
 
 def _check_shard(dpf, key, out, rank, world, n, alpha, bits=64):

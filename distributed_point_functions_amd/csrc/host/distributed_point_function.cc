@@ -309,6 +309,36 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   std::vector<dpf_block> seeds(std::max<int64_t>(n, 1));
   std::vector<uint8_t> ctrl(std::max<int64_t>(n, 1));
   if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
+    const int shift = stop_level - start_level;
+    auto parent_of = [&](int64_t i) -> uint128 { return shift < 128 ? prefixes[i] >> shift : 0; };
+    const auto& pe = ctx.partial_evaluations();
+    const int64_t m = pe.size();
+    // Sorted fast path (the usual hierarchical case: both the stored prefixes
+    // and the lookups come out of EvaluateUntil in ascending order): one merge
+    // pass instead of a hash map, with the reference's duplicate check
+    // (cc:365-383) on adjacent equal prefixes and its lookup error (cc:392-407).
+    bool sorted = true;
+    for (int64_t j = 1; j < m && sorted; ++j)
+      sorted = FromProtoBlock(pe[j - 1].prefix()) <= FromProtoBlock(pe[j].prefix());
+    for (int64_t i = 1; i < n && sorted; ++i) sorted = parent_of(i - 1) <= parent_of(i);
+    if (sorted) {
+      for (int64_t j = 1; j < m; ++j)
+        if (FromProtoBlock(pe[j - 1].prefix()) == FromProtoBlock(pe[j].prefix()) &&
+            (FromProtoBlock(pe[j - 1].seed()) != FromProtoBlock(pe[j].seed()) ||
+             pe[j - 1].control_bit() != pe[j].control_bit()))
+          return InvalidArgumentError(
+              "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
+      int64_t j = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        const uint128 want = parent_of(i);
+        while (j < m && FromProtoBlock(pe[j].prefix()) < want) ++j;
+        if (j == m || FromProtoBlock(pe[j].prefix()) != want)
+          return InvalidArgumentError("Prefix not present in ctx.partial_evaluations at hierarchy level " +
+                                      std::to_string(hierarchy_level));
+        seeds[i] = ToBlock(FromProtoBlock(pe[j].seed()));
+        ctrl[i] = pe[j].control_bit();
+      }
+    } else {
     std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> previous;
     previous.reserve(ctx.partial_evaluations_size() * 2);
     for (const PartialEvaluation& e : ctx.partial_evaluations()) {
@@ -327,6 +357,7 @@ Status DistributedPointFunction::ComputePartialEvaluations(
                                     std::to_string(hierarchy_level));
       seeds[i] = ToBlock(it->second.first);
       ctrl[i] = it->second.second;
+    }
     }
   } else {
     const dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
@@ -429,16 +460,29 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   if (num_prefixes > 0) {
     const int bib = parameters()[previous_hierarchy_level].log_domain_size() -
                     hierarchy_to_tree()[previous_hierarchy_level];
-    std::unordered_map<uint128, int64_t, U128Hash> inverse;
-    inverse.reserve(num_prefixes * 2);
     tree_indices.reserve(num_prefixes);
     prefix_map.reserve(num_prefixes);
-    for (int64_t i = 0; i < num_prefixes; ++i) {
-      uint128 ti = prefixes[i] >> bib;
-      int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
-      auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
-      if (inserted) tree_indices.push_back(ti);
-      prefix_map.emplace_back(it->second, bi);
+    bool ascending = true;
+    for (int64_t i = 1; i < num_prefixes && ascending; ++i) ascending = prefixes[i - 1] < prefixes[i];
+    if (ascending) {
+      // Ascending prefixes: equal tree indices are adjacent, first-seen order
+      // is sorted order -- no hash map needed.
+      for (int64_t i = 0; i < num_prefixes; ++i) {
+        uint128 ti = prefixes[i] >> bib;
+        int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
+        if (tree_indices.empty() || tree_indices.back() != ti) tree_indices.push_back(ti);
+        prefix_map.emplace_back(static_cast<int64_t>(tree_indices.size()) - 1, bi);
+      }
+    } else {
+      std::unordered_map<uint128, int64_t, U128Hash> inverse;
+      inverse.reserve(num_prefixes * 2);
+      for (int64_t i = 0; i < num_prefixes; ++i) {
+        uint128 ti = prefixes[i] >> bib;
+        int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
+        auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
+        if (inserted) tree_indices.push_back(ti);
+        prefix_map.emplace_back(it->second, bi);
+      }
     }
   }
 

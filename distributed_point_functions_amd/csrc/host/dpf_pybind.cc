@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "dpf/distributed_point_function.h"
+#include "synthetic_data_benchmarks.h"
 
 namespace py = pybind11;
 using namespace distributed_point_functions;
@@ -330,6 +331,47 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("packed_size", &PyDpf::PackedSize)
       .def("corrected_elements_per_block", &PyDpf::CorrectedElementsPerBlock)
       .def("output_elements", &PyDpf::OutputElements);
+  m.def("synthetic_levels", [](int log, int64_t count, double concentration, uint64_t seed, int mef) {
+    auto nz = experiments::MakeSyntheticNonzeros(count, log, concentration, seed);
+    auto prefixes = experiments::ComputePrefixes(nz, log);
+    auto levels = experiments::ComputeLevelsToEvaluate(prefixes, log, mef);
+    std::vector<int64_t> per_bit;
+    for (const auto& p : prefixes) per_bit.push_back(static_cast<int64_t>(p.size()));
+    py::array_t<uint64_t> a({static_cast<py::ssize_t>(nz.size()), py::ssize_t{2}});
+    if (!nz.empty()) std::memcpy(a.mutable_data(), nz.data(), nz.size() * 16);
+    return py::make_tuple(levels, per_bit, a);
+  });
+  m.def("run_synthetic_data_benchmark",
+        [](int log, int64_t count, double concentration, uint64_t seed, int mef, int iters,
+           bool only_nonzeros, bool verify) {
+          experiments::BenchmarkOptions o;
+          o.log_domain_size = log;
+          o.num_nonzeros = count;
+          o.concentration = concentration;
+          o.seed = seed;
+          o.max_expansion_factor = mef;
+          o.num_iterations = iters;
+          o.only_nonzeros = only_nonzeros;
+          o.verify = verify;
+          experiments::BenchmarkReport r;
+          {
+            py::gil_scoped_release nogil;
+            auto s = experiments::RunSyntheticDataBenchmark(o);
+            if (!s.ok()) {
+              py::gil_scoped_acquire g;
+              throw StatusError(s.status());
+            }
+            r = std::move(*s);
+          }
+          py::dict d;
+          d["levels_to_evaluate"] = r.levels_to_evaluate;
+          d["prefixes_per_level"] = r.prefixes_per_level;
+          d["outputs_per_level"] = r.outputs_per_level;
+          d["key_size_bytes"] = r.key_size_bytes;
+          d["seconds_per_iteration"] = r.seconds_per_iteration;
+          d["verified"] = r.verified;
+          return d;
+        });
   m.def("bits_needed", [](const py::bytes& vt, double sec) {
     return Take(dpf_internal::BitsNeeded(Parse<ValueType>(vt), sec));
   });
