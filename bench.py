@@ -49,8 +49,9 @@ KERNEL = "expand_kernel<FastIntLeaf<64, false> >"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 20; 1 for heavy_hitters, whose step is a full pass)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; 1)")
     ap.add_argument("--log-domain", type=int, default=LOG_PER_GPU,
                     help="log2 outputs per GPU (default 30 = the BASELINE config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,7 +59,7 @@ def parse():
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
     ap.add_argument("--workload", default="full_domain",
                     choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum",
-                             "synthetic_hierarchical", "synthetic_direct"],
+                             "synthetic_hierarchical", "synthetic_direct", "heavy_hitters"],
                     help="full_domain = BASELINE configs[1] (the headline); full_domain_u128 = "
                          "configs[2] (2^31 uint128 outputs per GPU, 2^34 over 8 GPUs); "
                          "evaluate_at(_sum) = configs[3] (2^20 keys x 2^10 points, log 128)")
@@ -67,7 +68,15 @@ def parse():
     ap.add_argument("--distribution", default="uniform", choices=["0.1", "0.5", "uniform"],
                     help="synthetic_*: 90%% of nonzeros in the first 10%%/50%% of the domain, or uniform")
     ap.add_argument("--points-log", type=int, default=10, help="evaluate_at: log2 points per key")
-    return ap.parse_args()
+    ap.add_argument("--top-k", type=int, default=1024,
+                    help="heavy_hitters: candidates kept per level (children = 4 x top-k)")
+    args = ap.parse_args()
+    long_step = args.workload == "heavy_hitters"
+    if args.steps is None:
+        args.steps = 1 if long_step else 20
+    if args.warmup is None:
+        args.warmup = 1 if long_step else 3
+    return args
 
 
 def tree_aes_per_launch(depth: int, blocks_needed: int = 1) -> int:
@@ -142,6 +151,8 @@ def main():
         return main_evaluate_at(args)
     if args.workload.startswith("synthetic"):
         return main_synthetic(args)
+    if args.workload == "heavy_hitters":
+        return main_heavy_hitters(args)
     if args.workload == "full_domain_u128" and args.log_domain == LOG_PER_GPU:
         args.log_domain = 31
     import torch
@@ -498,6 +509,166 @@ def main_synthetic(args):
         "outputs_per_s": outs / secs, "verified_two_server_reconstruction": r["verified"],
     }
     print(json.dumps(res), flush=True)
+
+
+HH_METRIC = ("heavy-hitters prefix evals/sec: 2^20 clients, 128-bit hierarchy {8,10,...,128}, "
+             "Tuple<IntModN32,IntModN32>, top-1024 candidates per level, both servers")
+
+
+def main_heavy_hitters(args):
+    """2^20 client keys per server, 61-level 128-bit
+    hierarchy, per level EvaluateUntil of every key at the <= 1024 current
+    candidates x 4 children, summed over keys on the device (device-resident
+    batch context), per-rank sums all-gathered (RCCL) and group-summed, the
+    two servers' sums added and the next candidates selected.  One step = one
+    full pass over all levels for BOTH servers; clients are split across ranks
+    (strong scaling)."""
+    import torch
+    import torch.distributed as dist
+    from distributed_point_functions_amd import dpf as D
+    from distributed_point_functions_amd import heavy_hitters as HH
+    from distributed_point_functions_amd import hip_abi as H
+    from distributed_point_functions_amd import sharding as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    H.load(require_gpu=True)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    logs = HH.hierarchy()
+    dpf = HH.create_dpf(logs)
+    n_keys = 1 << args.keys_log
+    values, idx, alphas = HH.client_values(n_keys, seed=0x5B)
+    lo, hi = S.key_range(n_keys, world, rank)
+    rng = np.random.default_rng(0x5B5B)
+    seeds = rng.integers(0, 2**64, size=(2 * n_keys, 2), dtype=np.uint64)
+    beta = D.to_value(HH.value_type(), HH.BETA)
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    b0, b1 = dpf.generate_key_batch(alphas[lo:hi], [beta] * len(logs),
+                                    root_seeds=seeds[2 * lo:2 * hi], threads=threads)
+    keygen_s = time.perf_counter() - t0
+    max_out = max(4 * args.top_k, 1 << logs[0])
+    servers = [HH.Server(dpf, dpf.upload_key_batch(b, stream=stream), max_out, dev)
+               for b in (b0, b1)]
+    aggregate = (lambda h, part, n: S.aggregate_shares(dpf, h, part, n)) if world > 1 else None
+    evs = []
+
+    class Timed:  # brackets every batched evaluation with hipEvents on `stream`
+        def __init__(self, srv):
+            self.srv, self.out = srv, srv.out
+
+        def evaluate(self, level, prefixes, stream=None):
+            a, b = H.Event(), H.Event()
+            a.record(stream)
+            n = self.srv.evaluate(level, prefixes, stream)
+            b.record(stream)
+            evs.append((a, b))
+            return n
+
+    def one_pass(record=None):
+        for srv in servers:
+            srv.reset()
+        return HH.run(dpf, [Timed(s) for s in servers], logs, args.top_k, aggregate, stream,
+                      record)
+
+    for _ in range(args.warmup):
+        one_pass()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs.clear()
+    record = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        final = one_pass(record if i == args.steps - 1 else None)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    kern_ms = sum(a.elapsed_ms(b) for a, b in evs) / args.steps
+    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+    if rank == 0:
+        HH.verify(record, logs, values, idx)        # every level, untimed
+    outputs_per_pass = sum(len(v) for _, v, _, _ in record) * n_keys * 2
+    aes_rank = HH.algorithmic_aes(dpf, logs, record, hi - lo) * 2
+    aes_total = HH.algorithmic_aes(dpf, logs, record, n_keys) * 2
+    achieved = aes_rank / (kern_ms_max * 1e-3) / 1e9
+    if rank == 0:
+        ref = HH.plaintext_prefix_counts(values, idx, 128)
+        true_top = set(sorted(ref, key=lambda v: (-ref[v], v))[:args.top_k])
+        res = {
+            "metric": HH_METRIC,
+            "value": outputs_per_pass * args.steps / elapsed,
+            "unit": "prefix evals/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32 mod N",
+            "data": "synthetic: 2^20 clients, values Zipf(1.1) over 2^14 random 128-bit values, "
+                    "key pairs from the product batched keygen (seeded), beta = (1, 7)",
+            "config": {"workload": f"heavy hitters, {n_keys} clients, {len(logs)} levels "
+                                   f"(log {logs[0]}..{logs[-1]} step 2), top-{args.top_k}, "
+                                   "EvaluateUntilBatchSumToDevice per level and server",
+                       "keys": n_keys, "levels": len(logs), "top_k": args.top_k,
+                       "parallelism": f"key-batch x{world}"},
+            "seconds_per_pass": elapsed / args.steps,
+            "outputs_per_pass": outputs_per_pass,
+            "aes_blocks_per_s": aes_total * args.steps / elapsed,
+            "keygen_s_rank0": keygen_s, "keygen_threads": threads,
+            "verified": "two-server reconstruction == plaintext prefix histogram at every level",
+            "true_top_k_recall": len(true_top & set(final)) / max(len(true_top), 1),
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
+                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
+                         "traffic": None, "kernel": "batch_level_kernel<Mod32V, 2, true>",
+                         "launch_ms_per_pass": kern_ms_max,
+                         "algorithmic_aes_per_pass": aes_rank},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_heavy_hitters(logs, record, alphas, seeds,
+                                                             args.top_k)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_heavy_hitters(logs, record, alphas, seeds, top_k, budget_s=15.0):
+    """The oracle's EvaluateUntil (C restatement of distributed_point_function.h:
+    641-837 + cc:351-498 over OpenSSL AES-NI, one host thread) on a bounded
+    sample of the workload: server 0's keys of the first clients, every level,
+    at the candidate prefixes the GPU run selected."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from distributed_point_functions_amd import heavy_hitters as HH
+    vt = ("tuple", [("intmodn", 32, HH.MODULUS)] * 2)
+    P = O.OracleParams([(log, vt, HH.SECURITY_PARAMETER) for log in logs])
+    plan, prev = [], []
+    for h, vals, counts, _ in record:
+        plan.append(prev)
+        prev = HH.select(vals, counts, top_k)
+    betas = [list(HH.BETA)] * len(logs)
+    dt, done, outs = 0.0, 0, 0
+    while dt < budget_s and done < len(alphas):
+        a = int(alphas[done, 0]) | int(alphas[done, 1]) << 64
+        k0, _ = O.generate_keys(P, a, betas, int(seeds[2 * done, 0]) | int(seeds[2 * done, 1]) << 64,
+                                int(seeds[2 * done + 1, 0]) | int(seeds[2 * done + 1, 1]) << 64)
+        ctx = O.create_context(P, k0)
+        t0 = time.perf_counter()
+        for h, pre in enumerate(plan):
+            outs += O.evaluate_until(P, h, pre, ctx).shape[0]
+        dt += time.perf_counter() - t0
+        done += 1
+    return {"value": outs / dt, "unit": "prefix evals/s", "cores": 1, "kind": "port",
+            "sample": f"{done} clients x all {len(logs)} levels of server 0 at the GPU run's "
+                      f"candidates (EvaluateUntil per key, oracle over OpenSSL AES-NI); "
+                      f"{dt:.1f} s on 1 host thread"}
 
 
 def _check_shard(dpf, key, out, rank, world, n, alpha, bits=64):

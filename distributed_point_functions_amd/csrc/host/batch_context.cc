@@ -1,0 +1,337 @@
+// batch_context.cc -- incremental evaluation of a whole key batch with a
+// device-resident EvaluationContext (config 5b, the
+// heavy-hitters hierarchy over 2^20 client keys).
+//
+// EvaluateUntilBatch*(h, prefixes, ctx) computes, for every key k of the batch,
+// exactly what EvaluateUntil<T>(h, prefixes, ctx_k)
+// (distributed_point_function.h:641-837) returns, and leaves the batch
+// context in the state the per-key contexts would be in:
+//   * validation and error messages of EvaluateUntil (h:655-700);
+//   * unique tree indices of the prefixes in first-seen order (h:718-742);
+//   * ComputePartialEvaluations (cc:351-453): each tree index is found under
+//     its parent among the stored partial evaluations (or walked from the
+//     root), walked down on the GPU, and stored as the new partial evaluation
+//     unless this is the last hierarchy level;
+//   * ExpandSeeds + HashExpandedSeeds + correction (cc:271-349, 500-524;
+//     h:745-808) and the per-prefix gather (h:817-836).
+// The host does O(#prefixes) bookkeeping per call; every per-key step runs in
+// one dpf_hip_eval_prefix_batch launch (csrc/kernels/dpf_batch.hip).
+#include <algorithm>
+#include <unordered_map>
+
+#include "dpf/distributed_point_function.h"
+#include "dpf/key_batch.h"
+#include "dpf_hip.h"
+#include "host_util.h"
+
+namespace distributed_point_functions {
+
+using dpf_internal::AesKey;
+using dpf_internal::FromBlock;
+using dpf_internal::FromHip;
+using dpf_internal::kPrgKeyLeft;
+using dpf_internal::kPrgKeyRight;
+using dpf_internal::kPrgKeyValue;
+using dpf_internal::MakeDesc;
+using dpf_internal::SetProtoBlock;
+using dpf_internal::ToBlock;
+using dpf_internal::U128Hash;
+
+Status DeviceBatchContext::Ensure(void** p, size_t* cap, size_t bytes) {
+  if (*p && *cap >= bytes) return OkStatus();
+  if (*p) dpf_hip_free(*p);
+  *p = nullptr;
+  *cap = 0;
+  const size_t want = std::max<size_t>(bytes, 256);
+  HIP_RETURN_IF_ERROR(dpf_hip_alloc(p, want));
+  *cap = want;
+  return OkStatus();
+}
+
+DeviceBatchContext::~DeviceBatchContext() {
+  for (void* p : {seeds_, ctrl_, next_seeds_, next_ctrl_, parent_, path_, save_, offsets_,
+                  workspace_, stage_, stage2_})
+    if (p) dpf_hip_free(p);
+}
+
+StatusOr<std::unique_ptr<DeviceBatchContext>> DistributedPointFunction::CreateBatchEvaluationContext(
+    const DeviceKeyBatch& keys) const {
+  if (keys.num_levels() != tree_levels_needed() - 1 ||
+      keys.num_hierarchy_levels() != static_cast<int>(parameters().size()))
+    return InvalidArgumentError("key batch does not match this DistributedPointFunction");
+  return std::unique_ptr<DeviceBatchContext>(new DeviceBatchContext(&keys));
+}
+
+StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchToDevice(
+    int hierarchy_level, Span<const uint128> prefixes, DeviceBatchContext& ctx, void* device_out,
+    int64_t capacity_bytes, void* stream) const {
+  return EvaluateUntilBatchCore(hierarchy_level, prefixes, ctx, false, device_out, capacity_bytes,
+                                stream);
+}
+
+StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchSumToDevice(
+    int hierarchy_level, Span<const uint128> prefixes, DeviceBatchContext& ctx, void* device_out,
+    int64_t capacity_bytes, void* stream) const {
+  return EvaluateUntilBatchCore(hierarchy_level, prefixes, ctx, true, device_out, capacity_bytes,
+                                stream);
+}
+
+StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
+    int hierarchy_level, Span<const uint128> prefixes, DeviceBatchContext& ctx, bool sum,
+    void* device_out, int64_t capacity_bytes, void* stream) const {
+  const DeviceKeyBatch& keys = ctx.keys();
+  const int H = static_cast<int>(parameters().size());
+  if (keys.num_levels() != tree_levels_needed() - 1 || keys.num_hierarchy_levels() != H)
+    return InvalidArgumentError("key batch does not match this DistributedPointFunction");
+  // h:655-700, in the reference's order.
+  if (hierarchy_level < 0 || hierarchy_level >= H)
+    return InvalidArgumentError(
+        "`hierarchy_level` must be non-negative and less than parameters_.size()");
+  if (hierarchy_level <= ctx.previous_hierarchy_level_)
+    return InvalidArgumentError(
+        "`hierarchy_level` must be greater than `ctx.previous_hierarchy_level`");
+  if ((ctx.previous_hierarchy_level_ < 0) != prefixes.empty())
+    return InvalidArgumentError(
+        "`prefixes` must be empty if and only if this is the first call with `ctx`.");
+  const int prev = ctx.previous_hierarchy_level_;
+  int prev_log = 0;
+  if (!prefixes.empty()) {
+    prev_log = parameters()[prev].log_domain_size();
+    for (uint128 prefix : prefixes)
+      if (prev_log < 128 && prefix >= (static_cast<uint128>(1) << prev_log))
+        return InvalidArgumentError("Index " + Uint128ToString(prefix) +
+                                    " out of range for hierarchy level " + std::to_string(prev));
+  }
+  const int log = parameters()[hierarchy_level].log_domain_size();
+  if (log - prev_log > 62)
+    return InvalidArgumentError(
+        "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
+
+  // Unique tree indices in first-seen order and each prefix's (tree index,
+  // block index) (h:718-742).
+  const int64_t P = static_cast<int64_t>(prefixes.size());
+  std::vector<uint128> tree_indices;
+  std::vector<std::pair<int64_t, int>> prefix_map;
+  if (P > 0) {
+    const int bib = prev_log - hierarchy_to_tree()[prev];
+    tree_indices.reserve(P);
+    prefix_map.reserve(P);
+    std::unordered_map<uint128, int64_t, U128Hash> inverse;
+    bool ascending = true;
+    for (int64_t i = 1; i < P && ascending; ++i) ascending = prefixes[i - 1] < prefixes[i];
+    if (!ascending) inverse.reserve(P * 2);
+    for (int64_t i = 0; i < P; ++i) {
+      const uint128 ti = prefixes[i] >> bib;
+      const int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
+      if (ascending) {
+        if (tree_indices.empty() || tree_indices.back() != ti) tree_indices.push_back(ti);
+        prefix_map.emplace_back(static_cast<int64_t>(tree_indices.size()) - 1, bi);
+      } else {
+        auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
+        if (inserted) tree_indices.push_back(ti);
+        prefix_map.emplace_back(it->second, bi);
+      }
+    }
+  }
+
+  // Where each tree index starts: a stored partial evaluation or the root
+  // (ExpandAndUpdateContext cc:455-498, ComputePartialEvaluations cc:351-453).
+  const int Dh = hierarchy_to_tree()[hierarchy_level];
+  int Dprev = 0, start_level = 0;
+  bool from_root = true;
+  std::vector<int32_t> parent_of;
+  if (P == 0) {
+    tree_indices.assign(1, 0);  // the root, expanded to depth Dh
+  } else {
+    Dprev = hierarchy_to_tree()[prev];
+    const auto& q = ctx.partial_prefixes_;
+    if (ctx.partial_evaluations_level_ >= 0 && !q.empty() &&
+        hierarchy_to_tree()[ctx.partial_evaluations_level_] <= Dprev) {
+      start_level = hierarchy_to_tree()[ctx.partial_evaluations_level_];
+      from_root = false;
+      const int shift = Dprev - start_level;
+      const bool sorted = std::is_sorted(q.begin(), q.end());
+      std::unordered_map<uint128, int32_t, U128Hash> pos;
+      if (!sorted) {
+        pos.reserve(q.size() * 2);
+        for (size_t j = 0; j < q.size(); ++j) pos.emplace(q[j], static_cast<int32_t>(j));
+      }
+      parent_of.resize(tree_indices.size());
+      for (size_t i = 0; i < tree_indices.size(); ++i) {
+        const uint128 want = shift < 128 ? tree_indices[i] >> shift : 0;
+        int64_t j = -1;
+        if (sorted) {
+          auto it = std::lower_bound(q.begin(), q.end(), want);
+          if (it != q.end() && *it == want) j = it - q.begin();
+        } else {
+          auto it = pos.find(want);
+          if (it != pos.end()) j = it->second;
+        }
+        if (j < 0)
+          return InvalidArgumentError(
+              "Prefix not present in ctx.partial_evaluations at hierarchy level " +
+              std::to_string(prev));
+        parent_of[i] = static_cast<int32_t>(j);
+      }
+    }
+  }
+  const int64_t T = static_cast<int64_t>(tree_indices.size());
+  const int W1 = Dprev - start_level;
+  const int dE = Dh - Dprev;
+
+  const auto& f = flat_[hierarchy_level];
+  const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
+  int max_e = dpf_hip_prefix_batch_max_expand(&desc, sum ? 1 : 0);
+  const bool native_sum = sum && max_e >= 0;
+  if (max_e < 0) max_e = dpf_hip_prefix_batch_max_expand(&desc, 0);
+  if (max_e < 0) return UnimplementedError("value type not supported by the batched GPU path");
+  const int E = std::min(dE, max_e);
+  const int s = dE - E;  // levels walked per start node below the tree index
+  if (s > 30 || (T << s) > INT32_MAX)
+    return ResourceExhaustedError(
+        "Too many start nodes for one batched evaluation; evaluate fewer levels at once.");
+  const int64_t U = T << s;
+  const int64_t K = keys.num_keys();
+  const int cepb = corrected_elements_per_block(hierarchy_level);
+  const int esz = f.packed_size;
+  const int64_t block = (int64_t{1} << dE) * cepb;   // elements per tree index
+  const int64_t n_blk = T * block;                  // elements per key before the gather
+  const int64_t cnt = int64_t{1} << (log - prev_log);  // elements per prefix
+  const int64_t n = P == 0 ? n_blk : P * cnt;
+  bool identity = P == 0 || (T == P && cnt == block);
+  for (int64_t i = 0; identity && P > 0 && i < P; ++i)
+    identity = prefix_map[i].first == i && prefix_map[i].second == 0;
+  const int64_t need = (sum ? n : K * n) * esz;
+  if (!device_out || capacity_bytes < need) return InvalidArgumentError("device output buffer too small");
+  const bool update_ctx = P > 0 && hierarchy_level < H - 1;
+
+  // Start-node tables: u = tree index i * 2^s + sub.
+  std::vector<int32_t> parent(U, 0), save(U, -1);
+  std::vector<dpf_block> path(U);
+  const uint128 w1_mask = W1 >= 128 ? ~uint128{0} : ((uint128{1} << W1) - 1);
+  for (int64_t i = 0; i < T; ++i) {
+    const uint128 low = tree_indices[i] & w1_mask;
+    for (int64_t sub = 0; sub < (int64_t{1} << s); ++sub) {
+      const int64_t u = (i << s) + sub;
+      if (!from_root) parent[u] = parent_of[i];
+      path[u] = ToBlock(s ? ((low << s) | static_cast<uint128>(sub)) : low);
+      if (sub == 0) save[u] = static_cast<int32_t>(i);
+    }
+  }
+  DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.parent_, &ctx.parent_cap_, U * sizeof(int32_t)));
+  DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.path_, &ctx.path_cap_, U * sizeof(dpf_block)));
+  DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.save_, &ctx.save_cap_, U * sizeof(int32_t)));
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.parent_, parent.data(), U * sizeof(int32_t), stream));
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.path_, path.data(), U * sizeof(dpf_block), stream));
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.save_, save.data(), U * sizeof(int32_t), stream));
+  if (update_ctx) {
+    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.next_seeds_, &ctx.next_seeds_cap_,
+                                                   K * T * sizeof(dpf_block)));
+    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.next_ctrl_, &ctx.next_ctrl_cap_, K * T));
+  }
+  std::vector<int64_t> offsets;
+  if (!identity) {
+    offsets.resize(P);
+    for (int64_t i = 0; i < P; ++i)
+      offsets[i] = prefix_map[i].first * block + prefix_map[i].second * cnt;
+    DPF_RETURN_IF_ERROR(
+        DeviceBatchContext::Ensure(&ctx.offsets_, &ctx.offsets_cap_, P * sizeof(int64_t)));
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.offsets_, offsets.data(), P * sizeof(int64_t), stream));
+  }
+
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  auto launch = [&](int sum_mode, void* out, uint64_t* workspace) {
+    return FromHip(dpf_hip_eval_prefix_batch(
+        K, U, W1 + s, update_ctx ? W1 : -1, E, start_level, keys.num_levels(), keys.seed(),
+        keys.party(), from_root ? nullptr : ctx.partial_seeds(),
+        from_root ? nullptr : ctx.partial_control(), static_cast<int64_t>(ctx.partial_prefixes_.size()),
+        static_cast<const int32_t*>(ctx.parent_), static_cast<const dpf_block*>(ctx.path_),
+        static_cast<const int32_t*>(ctx.save_), static_cast<dpf_block*>(ctx.next_seeds_),
+        static_cast<uint8_t*>(ctx.next_ctrl_), T, keys.cw_seed(), keys.cw_left(), keys.cw_right(),
+        &kl, &kr, &kv, &desc, cepb, keys.value_correction(hierarchy_level), sum_mode, workspace,
+        out, stream));
+  };
+  if (native_sum) {
+    void* target = device_out;
+    if (!identity) {
+      DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage_, &ctx.stage_cap_, n_blk * esz));
+      target = ctx.stage_;
+    }
+    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(
+        &ctx.workspace_, &ctx.workspace_cap_, n_blk * f.leaves.size() * 3 * sizeof(uint64_t)));
+    DPF_RETURN_IF_ERROR(launch(1, target, static_cast<uint64_t*>(ctx.workspace_)));
+    if (!identity)
+      HIP_RETURN_IF_ERROR(dpf_hip_gather(P, cnt, esz, static_cast<const int64_t*>(ctx.offsets_),
+                                         ctx.stage_, device_out, stream));
+  } else if (sum) {
+    // Value types without an on-device key sum in the kernel: per-key rows,
+    // then a group sum over the rows.
+    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage_, &ctx.stage_cap_, K * n_blk * esz));
+    DPF_RETURN_IF_ERROR(launch(0, ctx.stage_, nullptr));
+    void* target = device_out;
+    if (!identity) {
+      DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage2_, &ctx.stage2_cap_, n_blk * esz));
+      target = ctx.stage2_;
+    }
+    HIP_RETURN_IF_ERROR(dpf_hip_sum_rows(K, n_blk, &desc, ctx.stage_, target, stream));
+    if (!identity)
+      HIP_RETURN_IF_ERROR(dpf_hip_gather(P, cnt, esz, static_cast<const int64_t*>(ctx.offsets_),
+                                         ctx.stage2_, device_out, stream));
+  } else {
+    void* target = device_out;
+    if (!identity) {
+      DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage_, &ctx.stage_cap_, K * n_blk * esz));
+      target = ctx.stage_;
+    }
+    DPF_RETURN_IF_ERROR(launch(0, target, nullptr));
+    if (!identity)
+      HIP_RETURN_IF_ERROR(dpf_hip_gather_batched(K, n_blk, P, cnt, esz,
+                                                 static_cast<const int64_t*>(ctx.offsets_),
+                                                 ctx.stage_, device_out, stream));
+  }
+
+  // Context update (cc:435-451, 494-496).
+  ctx.previous_hierarchy_level_ = hierarchy_level;
+  if (P > 0) {
+    if (update_ctx) {
+      ctx.partial_prefixes_ = std::move(tree_indices);
+      std::swap(ctx.seeds_, ctx.next_seeds_);
+      std::swap(ctx.seeds_cap_, ctx.next_seeds_cap_);
+      std::swap(ctx.ctrl_, ctx.next_ctrl_);
+      std::swap(ctx.ctrl_cap_, ctx.next_ctrl_cap_);
+    } else {
+      ctx.partial_prefixes_.clear();
+    }
+    ctx.partial_evaluations_level_ = prev;
+  }
+  return n;
+}
+
+StatusOr<EvaluationContext> DistributedPointFunction::ExportEvaluationContext(
+    const DeviceBatchContext& ctx, const KeyBatch& host_keys, int64_t k, void* stream) const {
+  const DeviceKeyBatch& keys = ctx.keys();
+  if (k < 0 || k >= keys.num_keys()) return InvalidArgumentError("key index out of range");
+  DPF_ASSIGN_OR_RETURN(DpfKey key, KeyFromBatch(host_keys, keys.first_key() + k));
+  DPF_ASSIGN_OR_RETURN(EvaluationContext out, CreateEvaluationContext(std::move(key)));
+  out.set_previous_hierarchy_level(ctx.previous_hierarchy_level());
+  if (ctx.partial_evaluations_level() >= 0)
+    out.set_partial_evaluations_level(ctx.partial_evaluations_level());
+  const auto& q = ctx.partial_prefixes();
+  if (!q.empty()) {
+    const int64_t Q = static_cast<int64_t>(q.size());
+    std::vector<dpf_block> seeds(Q);
+    std::vector<uint8_t> ctrl(Q);
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds.data(), ctx.partial_seeds() + k * Q,
+                                           Q * sizeof(dpf_block), stream));
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(ctrl.data(), ctx.partial_control() + k * Q, Q, stream));
+    for (int64_t i = 0; i < Q; ++i) {
+      PartialEvaluation* e = out.add_partial_evaluations();
+      SetProtoBlock(q[i], e->mutable_prefix());
+      SetProtoBlock(FromBlock(seeds[i]), e->mutable_seed());
+      e->set_control_bit(ctrl[i] != 0);
+    }
+  }
+  return out;
+}
+
+}  // namespace distributed_point_functions

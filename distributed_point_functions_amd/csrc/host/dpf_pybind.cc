@@ -96,6 +96,17 @@ struct PyDeviceKeyBatch {
   int64_t FirstKey() const { return d->first_key(); }
 };
 
+// Holds the device key batch alive as long as its context.
+struct PyBatchContext {
+  std::shared_ptr<DeviceKeyBatch> keys;
+  std::shared_ptr<DeviceBatchContext> ctx;
+  int PreviousHierarchyLevel() const { return ctx->previous_hierarchy_level(); }
+  int PartialEvaluationsLevel() const { return ctx->partial_evaluations_level(); }
+  int64_t NumPartialEvaluations() const {
+    return static_cast<int64_t>(ctx->partial_prefixes().size());
+  }
+};
+
 class PyDpf {
  public:
   static PyDpf CreateIncremental(const std::vector<py::bytes>& params) {
@@ -263,6 +274,33 @@ class PyDpf {
       throw StatusError(st);
     }
   }
+  PyBatchContext CreateBatchEvaluationContext(const PyDeviceKeyBatch& keys) {
+    auto c = Take(dpf_->CreateBatchEvaluationContext(*keys.d));
+    return PyBatchContext{keys.d, std::shared_ptr<DeviceBatchContext>(c.release())};
+  }
+  int64_t EvaluateUntilBatchToDevice(int level,
+                                     const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& prefixes,
+                                     PyBatchContext& ctx, bool sum, uintptr_t out, int64_t capacity,
+                                     uintptr_t stream) {
+    auto p = ToU128(prefixes);
+    py::gil_scoped_release nogil;
+    auto r = sum ? dpf_->EvaluateUntilBatchSumToDevice(level, MakeConstSpan(p), *ctx.ctx,
+                                                       reinterpret_cast<void*>(out), capacity,
+                                                       reinterpret_cast<void*>(stream))
+                 : dpf_->EvaluateUntilBatchToDevice(level, MakeConstSpan(p), *ctx.ctx,
+                                                    reinterpret_cast<void*>(out), capacity,
+                                                    reinterpret_cast<void*>(stream));
+    if (!r.ok()) {
+      py::gil_scoped_acquire g;
+      throw StatusError(r.status());
+    }
+    return *r;
+  }
+  py::bytes ExportEvaluationContext(const PyBatchContext& ctx, const PyKeyBatch& host, int64_t k,
+                                    uintptr_t stream) {
+    return Ser(Take(dpf_->ExportEvaluationContext(*ctx.ctx, *host.b, k,
+                                                  reinterpret_cast<void*>(stream))));
+  }
   py::array_t<uint8_t> SumPackedShares(int level, const py::array_t<uint8_t, py::array::c_style>& shares,
                                        int64_t num_shares, int64_t count) {
     if (static_cast<int64_t>(shares.size()) != num_shares * count * dpf_->flat_value_type(level).packed_size)
@@ -296,6 +334,11 @@ PYBIND11_MODULE(_dpf_host, m) {
   py::class_<PyDeviceKeyBatch>(m, "DeviceKeyBatch")
       .def_property_readonly("num_keys", &PyDeviceKeyBatch::NumKeys)
       .def_property_readonly("first_key", &PyDeviceKeyBatch::FirstKey);
+  py::class_<PyBatchContext>(m, "DeviceBatchContext")
+      .def_property_readonly("previous_hierarchy_level", &PyBatchContext::PreviousHierarchyLevel)
+      .def_property_readonly("partial_evaluations_level", &PyBatchContext::PartialEvaluationsLevel)
+      .def_property_readonly("num_partial_evaluations", &PyBatchContext::NumPartialEvaluations)
+      .def("reset", [](PyBatchContext& c) { c.ctx->Reset(); });
   py::class_<PyKeyBatch>(m, "KeyBatch")
       .def_property_readonly("num_keys", &PyKeyBatch::NumKeys)
       .def_property_readonly("num_levels", &PyKeyBatch::NumLevels)
@@ -322,6 +365,9 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("generate_key_batch", &PyDpf::GenerateKeyBatch)
       .def("evaluate_at_batch_to_device", &PyDpf::EvaluateAtBatchToDevice)
       .def("evaluate_at_batch_sum_to_device", &PyDpf::EvaluateAtBatchSumToDevice)
+      .def("create_batch_evaluation_context", &PyDpf::CreateBatchEvaluationContext)
+      .def("evaluate_until_batch_to_device", &PyDpf::EvaluateUntilBatchToDevice)
+      .def("export_evaluation_context", &PyDpf::ExportEvaluationContext)
       .def("sum_packed_shares", &PyDpf::SumPackedShares)
       .def("parameters", &PyDpf::Parameters)
       .def("tree_levels_needed", &PyDpf::TreeLevelsNeeded)

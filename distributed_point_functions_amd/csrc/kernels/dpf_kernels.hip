@@ -27,15 +27,10 @@
 #include <string>
 
 #include "../../../include/dpf_hip.h"
-#include "aes_core.h"
+#include "dpf_device.h"
+#include "dpf_runtime.h"
 
-namespace {
-
-// ------------------------------------------------------------------------
-// Status plumbing (absl codes)
-// ------------------------------------------------------------------------
-constexpr int kOk = 0, kInvalidArgument = 3, kResourceExhausted = 8, kUnimplemented = 12,
-              kInternal = 13;
+namespace dpf_rt {
 thread_local std::string g_last_error;
 
 int fail(int code, const std::string& msg) {
@@ -46,410 +41,11 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(e == hipErrorOutOfMemory ? kResourceExhausted : kInternal,
               std::string(what) + ": " + hipGetErrorString(e));
 }
-#define HIP_TRY(expr)                                   \
-  do {                                                  \
-    hipError_t _e = (expr);                             \
-    if (_e != hipSuccess) return hip_fail(_e, #expr);   \
-  } while (0)
+}  // namespace dpf_rt
 
-// ------------------------------------------------------------------------
-// Tables and keys
-// ------------------------------------------------------------------------
-struct T0Table {
-  uint32_t v[256];
-};
-constexpr T0Table make_t0() {
-  T0Table t{};
-  for (int i = 0; i < 256; ++i) {
-    uint32_t s = dpf_aes::kSbox[i];
-    uint32_t s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
-    t.v[i] = s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
-  }
-  return t;
-}
-__constant__ T0Table c_t0 = make_t0();
+using namespace dpf_rt;
 
-struct RoundKeys {
-  uint32_t k[44];
-};
-
-RoundKeys expand_key(const dpf_aes_key* key) {
-  RoundKeys rk;
-  dpf_aes::expand_key(key->bytes, rk.k);
-  return rk;
-}
-
-constexpr int kBlock = 1024;             // threads per workgroup (16 waves)
-constexpr int kTabWords = 4 * 256 * 32;  // 4 tables x 256 entries x 32 bank copies = 128 KiB
-constexpr int kMaxCwLevels = 128;
-constexpr int kSMax = 12;                // max subtree depth handled per thread
-constexpr int kGMax = kSMax - 1;         // max depth of the DFS stack above leaf pairs
-constexpr int kBMax = 8;                 // max AES blocks hashed per leaf (generic path)
-
-// LDS image: [tables 128 KiB][cw seeds 128 x 16 B][cw control 128 x 4 B]
-struct LdsImage {
-  uint32_t tab[kTabWords];
-  uint4 cw_seed[kMaxCwLevels];
-  uint32_t cw_ctrl[kMaxCwLevels];
-};
-
-// Table image: 256-byte rows.  Row e of the low 64 KiB = [T0[e] x 32 copies |
-// T1[e] x 32 copies], of the high 64 KiB = [T2[e] x 32 | T3[e] x 32].  Lane l
-// reads copy (l & 31), so every ds_read_b32 of a wave is bank-conflict-free.
-__device__ __forceinline__ void fill_tables(uint32_t* tab) {
-  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) {
-    int t = 2 * (i >> 14) + ((i >> 5) & 1), e = (i >> 6) & 255;
-    uint32_t v = c_t0.v[e];
-    tab[i] = t == 0 ? v : ((v << (8 * t)) | (v >> (32 - 8 * t)));
-  }
-}
-
-__device__ __forceinline__ void fill_cws(LdsImage& lds, const dpf_block* cw_seed,
-                                         const uint8_t* cw_left, const uint8_t* cw_right,
-                                         int num_levels) {
-  for (int i = threadIdx.x; i < num_levels; i += blockDim.x) {
-    dpf_block b = cw_seed[i];
-    lds.cw_seed[i] = make_uint4((uint32_t)b.low, (uint32_t)(b.low >> 32), (uint32_t)b.high,
-                                (uint32_t)(b.high >> 32));
-    lds.cw_ctrl[i] = (uint32_t)(cw_left[i] & 1) | ((uint32_t)(cw_right[i] & 1) << 1);
-  }
-}
-
-// Conflict-free LDS T-table lookup with ONE VALU of addressing: v_perm_b32
-// builds the byte address {lane offset, byte K of w, table half, 0}, i.e.
-// (entry << 8) | lt[T] with lt[T] = (lane & 31) * 4 (+128 for T1/T3, +64 KiB
-// for T2/T3).
-struct LdsLookup {
-  const char* base;
-  uint32_t lt[4];
-  template <int T, int K>
-  __device__ __forceinline__ uint32_t lookup(uint32_t w) const {
-    constexpr uint32_t sel = 0x0c020000u | ((4u + K) << 8);
-    uint32_t off = __builtin_amdgcn_perm(w, lt[T], sel);
-    return *reinterpret_cast<const uint32_t*>(base + off);
-  }
-  __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) const {
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-  }
-};
-
-__device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds) {
-  uint32_t l = (threadIdx.x & 31) * 4u;
-  return LdsLookup{reinterpret_cast<const char*>(lds.tab), {l, l + 128u, l + 65536u, l + 65664u}};
-}
-
-// Round keys shared by the whole wave (kernel-argument resident).
-struct UniformRK {
-  const uint32_t* k;
-  __device__ __forceinline__ uint32_t operator()(int i) const { return k[i]; }
-};
-// Per-lane key choice: rk = left ^ (mask & (left ^ right)).
-struct SelectRK {
-  const uint32_t* left;
-  const uint32_t* diff;
-  uint32_t mask;
-  __device__ __forceinline__ uint32_t operator()(int i) const { return left[i] ^ (mask & diff[i]); }
-};
-
-using dpf_aes::Block4;
-
-__device__ __forceinline__ Block4 load_block(const dpf_block* p) {
-  uint4 v = *reinterpret_cast<const uint4*>(p);
-  return Block4{v.x, v.y, v.z, v.w};
-}
-__device__ __forceinline__ void store_block(dpf_block* p, Block4 b) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(b.w0, b.w1, b.w2, b.w3);
-}
-__device__ __forceinline__ Block4 add_small(Block4 s, uint32_t j) {
-  // seed + j as absl::uint128 (distributed_point_function.cc:512)
-  uint64_t lo = ((uint64_t)s.w1 << 32) | s.w0, hi = ((uint64_t)s.w3 << 32) | s.w2;
-  uint64_t nlo = lo + j;
-  hi += (nlo < lo) ? 1 : 0;
-  return Block4{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-}
-
-// One tree step for a uniformly chosen child: seed/control correction and
-// control-bit extraction in the order of distributed_point_function.cc:323-343.
-__device__ __forceinline__ void child_step(const LdsLookup& lk, const uint32_t* rk, Block4 s,
-                                           uint32_t t, uint32_t dir, uint4 cs, uint32_t cctl,
-                                           Block4& out, uint32_t& tout) {
-  Block4 h = dpf_aes::mmo_hash(s, lk, UniformRK{rk});
-  uint32_t m = 0u - t;
-  h.w0 ^= cs.x & m; h.w1 ^= cs.y & m; h.w2 ^= cs.z & m; h.w3 ^= cs.w & m;
-  uint32_t nt = h.w0 & 1u;
-  h.w0 &= ~1u;
-  nt ^= t & ((cctl >> dir) & 1u);
-  out = h;
-  tout = nt;
-}
-
-// Both children of one node: two interleaved MMO hashes (left key, right key).
-__device__ __forceinline__ void children_step(const LdsLookup& lk, const uint32_t* rkl,
-                                              const uint32_t* rkr, Block4 s, uint32_t t, uint4 cs,
-                                              uint32_t cctl, Block4& c0, uint32_t& t0, Block4& c1,
-                                              uint32_t& t1) {
-  Block4 h0 = s, h1 = s;
-  dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{rkl}, UniformRK{rkr});
-  uint32_t m = 0u - t;
-  h0.w0 ^= cs.x & m; h0.w1 ^= cs.y & m; h0.w2 ^= cs.z & m; h0.w3 ^= cs.w & m;
-  h1.w0 ^= cs.x & m; h1.w1 ^= cs.y & m; h1.w2 ^= cs.z & m; h1.w3 ^= cs.w & m;
-  t0 = (h0.w0 & 1u) ^ (t & (cctl & 1u));
-  t1 = (h1.w0 & 1u) ^ (t & ((cctl >> 1) & 1u));
-  h0.w0 &= ~1u;
-  h1.w0 &= ~1u;
-  c0 = h0;
-  c1 = h1;
-}
-
-// Path step with a per-lane direction bit (evaluate_prg_hwy.cc:452-486).
-__device__ __forceinline__ void path_step(const LdsLookup& lk, const RoundKeys& rkl,
-                                          const RoundKeys& rkd, Block4& s, uint32_t& t,
-                                          uint32_t bit, uint4 cs, uint32_t cctl) {
-  Block4 h = dpf_aes::mmo_hash(s, lk, SelectRK{rkl.k, rkd.k, 0u - bit});
-  uint32_t m = 0u - t;
-  h.w0 ^= cs.x & m; h.w1 ^= cs.y & m; h.w2 ^= cs.z & m; h.w3 ^= cs.w & m;
-  uint32_t nt = h.w0 & 1u;
-  h.w0 &= ~1u;
-  nt ^= t & ((cctl >> bit) & 1u);
-  s = h;
-  t = nt;
-}
-
-// ------------------------------------------------------------------------
-// Leaf conversion + correction (a12/a13)
-// ------------------------------------------------------------------------
-
-// Element-wise add/neg of a 128-bit block viewed as 128/BITS little-endian lanes.
-template <int BITS>
-__device__ __forceinline__ Block4 lanes_add(Block4 a, Block4 b) {
-  if constexpr (BITS == 128) {
-    uint64_t alo = ((uint64_t)a.w1 << 32) | a.w0, ahi = ((uint64_t)a.w3 << 32) | a.w2;
-    uint64_t blo = ((uint64_t)b.w1 << 32) | b.w0, bhi = ((uint64_t)b.w3 << 32) | b.w2;
-    uint64_t lo = alo + blo, hi = ahi + bhi + (lo < alo ? 1 : 0);
-    return Block4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-  } else if constexpr (BITS == 64) {
-    uint64_t lo = (((uint64_t)a.w1 << 32) | a.w0) + (((uint64_t)b.w1 << 32) | b.w0);
-    uint64_t hi = (((uint64_t)a.w3 << 32) | a.w2) + (((uint64_t)b.w3 << 32) | b.w2);
-    return Block4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-  } else if constexpr (BITS == 32) {
-    return Block4{a.w0 + b.w0, a.w1 + b.w1, a.w2 + b.w2, a.w3 + b.w3};
-  } else {
-    constexpr uint32_t H = BITS == 16 ? 0x80008000u : 0x80808080u;
-    auto f = [](uint32_t x, uint32_t y) { return ((x & ~H) + (y & ~H)) ^ ((x ^ y) & H); };
-    return Block4{f(a.w0, b.w0), f(a.w1, b.w1), f(a.w2, b.w2), f(a.w3, b.w3)};
-  }
-}
-template <int BITS>
-__device__ __forceinline__ Block4 lanes_neg(Block4 a) {
-  if constexpr (BITS == 128) {
-    uint64_t lo = ((uint64_t)a.w1 << 32) | a.w0, hi = ((uint64_t)a.w3 << 32) | a.w2;
-    uint64_t nlo = 0 - lo, nhi = 0 - hi - (lo != 0 ? 1 : 0);
-    return Block4{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
-  } else if constexpr (BITS == 64) {
-    uint64_t lo = 0 - (((uint64_t)a.w1 << 32) | a.w0);
-    uint64_t hi = 0 - (((uint64_t)a.w3 << 32) | a.w2);
-    return Block4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-  } else if constexpr (BITS == 32) {
-    return Block4{0u - a.w0, 0u - a.w1, 0u - a.w2, 0u - a.w3};
-  } else {
-    constexpr uint32_t H = BITS == 16 ? 0x80008000u : 0x80808080u;
-    auto f = [](uint32_t x) { return (H - (x & ~H)) ^ (~x & H); };
-    return Block4{f(a.w0), f(a.w1), f(a.w2), f(a.w3)};
-  }
-}
-
-// Plain unsigned integers and XorWrapper of them with b == 1: the hashed block
-// *is* the element array (value_type_helpers.h:199-211), the correction word is
-// one block in the same layout.
-template <int BITS, bool XOR>
-struct FastIntLeaf {
-  const dpf_block* vcw_elems;  // E elements, one dpf_block each (device)
-  int E;
-  int party;
-  int store_bytes;    // elements_per_leaf * BITS / 8 (1..16)
-  Block4 vcw;         // value correction packed as E lanes of BITS (set by init)
-
-  // Packs the per-element correction into one block (value_type_helpers.h:597-631
-  // produces E elements whose concatenation has the hashed block's layout).
-  __device__ __forceinline__ void init() {
-    unsigned __int128 packed = 0;
-    for (int e = E - 1; e >= 0; --e) {
-      dpf_block c = vcw_elems[e];
-      unsigned __int128 v = ((unsigned __int128)c.high << 64) | c.low;
-      if (BITS < 128) {
-        v &= (((unsigned __int128)1 << (BITS & 127)) - 1);
-        packed = (packed << (BITS & 127)) | v;
-      } else {
-        packed = v;
-      }
-    }
-    vcw = Block4{(uint32_t)packed, (uint32_t)(packed >> 32), (uint32_t)(packed >> 64),
-                 (uint32_t)(packed >> 96)};
-  }
-
-  __device__ __forceinline__ Block4 correct(Block4 h, uint32_t t) const {
-    if (XOR) {
-      uint32_t m = 0u - t;
-      return Block4{h.w0 ^ (vcw.w0 & m), h.w1 ^ (vcw.w1 & m), h.w2 ^ (vcw.w2 & m),
-                    h.w3 ^ (vcw.w3 & m)};
-    }
-    if (t) h = lanes_add<BITS>(h, vcw);
-    if (party == 1) h = lanes_neg<BITS>(h);
-    return h;
-  }
-
-  __device__ __forceinline__ void store(Block4 h, int64_t leaf, char* out) const {
-    char* p = out + leaf * (int64_t)store_bytes;
-    switch (store_bytes) {
-      case 16: *reinterpret_cast<uint4*>(p) = make_uint4(h.w0, h.w1, h.w2, h.w3); break;
-      case 8: *reinterpret_cast<uint2*>(p) = make_uint2(h.w0, h.w1); break;
-      case 4: *reinterpret_cast<uint32_t*>(p) = h.w0; break;
-      case 2: *reinterpret_cast<uint16_t*>(p) = (uint16_t)h.w0; break;
-      default: *reinterpret_cast<uint8_t*>(p) = (uint8_t)h.w0; break;
-    }
-  }
-
-  // Full-domain leaf: write elements_per_leaf elements.
-  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
-                                       uint32_t t, int64_t leaf, char* out) const {
-    store(correct(dpf_aes::mmo_hash(seed, lk, UniformRK{rkv}), t), leaf, out);
-  }
-  // Two sibling leaves (leaf, leaf + 1), hashed as one interleaved pair.
-  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
-                                        uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
-                                        char* out) const {
-    dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{rkv}, UniformRK{rkv});
-    s0 = correct(s0, t0);
-    s1 = correct(s1, t1);
-    if (store_bytes == 16) {
-      uint4* p = reinterpret_cast<uint4*>(out + leaf * 16);
-      p[0] = make_uint4(s0.w0, s0.w1, s0.w2, s0.w3);
-      p[1] = make_uint4(s1.w0, s1.w1, s1.w2, s1.w3);
-    } else {
-      store(s0, leaf, out);
-      store(s1, leaf + 1, out);
-    }
-  }
-};
-
-// Descriptor-driven conversion for Tuple / IntModN / multi-block types
-// (value_type_helpers.h:286-311, 415-443, 526-589).
-struct GenericLeaf {
-  dpf_value_desc d;
-  const dpf_block* vcw;   // E * num_leaves blocks
-  int party;
-  int elements_per_leaf;  // full domain: corrected elements per block
-  int esz;                // packed element size in bytes
-
-  __device__ __forceinline__ void init() {}
-
-  __device__ static unsigned __int128 load_le(const uint8_t* p, int n) {
-    unsigned __int128 v = 0;
-    for (int i = n - 1; i >= 0; --i) v = (v << 8) | p[i];
-    return v;
-  }
-  __device__ static unsigned __int128 mask(int bits) {
-    return bits >= 128 ? ~(unsigned __int128)0 : (((unsigned __int128)1 << bits) - 1);
-  }
-  __device__ unsigned __int128 modulus(int k) const {
-    return ((unsigned __int128)d.mod_high[k] << 64) | d.mod_low[k];
-  }
-  __device__ unsigned __int128 add(int k, unsigned __int128 a, unsigned __int128 b) const {
-    if (d.kind[k] == DPF_LEAF_XOR) return a ^ b;
-    if (d.kind[k] == DPF_LEAF_INTMODN) {
-      // IntModN += (int_mod_n.h:116-120, 208-223)
-      unsigned __int128 n = modulus(k), c = n - b;
-      return a >= c ? a - c : n - c + a;
-    }
-    return (a + b) & mask(d.bits[k]);
-  }
-  __device__ unsigned __int128 neg(int k, unsigned __int128 a) const {
-    if (d.kind[k] == DPF_LEAF_XOR) return a;
-    if (d.kind[k] == DPF_LEAF_INTMODN) return a == 0 ? 0 : modulus(k) - a;
-    return (0 - a) & mask(d.bits[k]);
-  }
-  __device__ static void store_le(char* p, unsigned __int128 v, int n) {
-    for (int i = 0; i < n; ++i) { p[i] = (char)(uint8_t)v; v >>= 8; }
-  }
-
-  // Hashes `seed` into b blocks and writes element `first .. first+count` of the
-  // converted array (after correction) to out_elem.
-  __device__ void convert_store(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
-                                uint32_t t, int first, int count, char* out_elem) const {
-    uint8_t bytes[16 * kBMax];
-    const int b = d.blocks_needed;
-    for (int j = 0; j < b; ++j) {
-      Block4 h = dpf_aes::mmo_hash(add_small(seed, (uint32_t)j), lk, UniformRK{rkv});
-      uint32_t w[4] = {h.w0, h.w1, h.w2, h.w3};
-      for (int q = 0; q < 16; ++q) bytes[16 * j + q] = (uint8_t)(w[q >> 2] >> (8 * (q & 3)));
-    }
-    const int nl = d.num_leaves;
-    if (d.direct) {
-      for (int e = first; e < first + count; ++e) {
-        int off = e * esz;
-        char* o = out_elem + (e - first) * esz;
-        for (int k = 0; k < nl; ++k) {
-          int lb = d.bits[k] >> 3;
-          unsigned __int128 v = load_le(bytes + off, lb);
-          if (t) {
-            dpf_block c = vcw[e * nl + k];
-            v = add(k, v, ((unsigned __int128)c.high << 64) | c.low);
-          }
-          if (party == 1) v = neg(k, v);
-          store_le(o, v, lb);
-          o += lb;
-          off += lb;
-        }
-      }
-      return;
-    }
-    // Sampling conversion: E == 1, every leaf but the last refills the block.
-    unsigned __int128 block = load_le(bytes, 16);
-    int rem = 16;
-    char* o = out_elem;
-    for (int k = 0; k < nl; ++k) {
-      int lb = d.bits[k] >> 3;
-      bool update = k + 1 < nl;
-      unsigned __int128 v;
-      if (d.kind[k] == DPF_LEAF_INTMODN) {
-        unsigned __int128 n = modulus(k);
-        unsigned __int128 q = block / n;
-        v = block - q * n;
-        if (update) {
-          block = lb < 16 ? (q << (8 * lb)) : 0;
-          block |= load_le(bytes + rem, lb);
-          rem += lb;
-        }
-      } else {
-        v = block & mask(d.bits[k]);
-        if (update) {
-          if (lb < 16) block &= ~mask(d.bits[k]); else block = 0;
-          block |= load_le(bytes + rem, lb);
-          rem += lb;
-        }
-      }
-      if (t) {
-        dpf_block c = vcw[k];
-        v = add(k, v, ((unsigned __int128)c.high << 64) | c.low);
-      }
-      if (party == 1) v = neg(k, v);
-      store_le(o, v, lb);
-      o += lb;
-    }
-  }
-
-  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
-                                       uint32_t t, int64_t leaf, char* out) const {
-    convert_store(lk, rkv, seed, t, 0, elements_per_leaf,
-                  out + leaf * (int64_t)elements_per_leaf * esz);
-  }
-  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
-                                        uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
-                                        char* out) const {
-    emit(lk, rkv, s0, t0, leaf, out);
-    emit(lk, rkv, s1, t1, leaf + 1, out);
-  }
-};
+namespace {
 
 // ------------------------------------------------------------------------
 // Kernels
@@ -482,10 +78,6 @@ struct PathParams {
   RoundKeys rkl, rkd;
 };
 
-__device__ __forceinline__ uint32_t path_bit(Block4 p, int pos) {
-  uint32_t w = pos < 32 ? p.w0 : pos < 64 ? p.w1 : pos < 96 ? p.w2 : p.w3;
-  return (w >> (pos & 31)) & 1u;
-}
 
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void eval_paths_kernel(PathParams p) {
   __shared__ LdsImage lds;
@@ -622,112 +214,6 @@ struct PointParams {
   RoundKeys rkl, rkd, rkv;
 };
 
-// Two path steps with per-lane directions, interleaved (evaluate_prg_hwy.cc:452-486).
-__device__ __forceinline__ void path_step2(const LdsLookup& lk, const RoundKeys& rkl,
-                                           const RoundKeys& rkd, Block4& s0, uint32_t& t0,
-                                           uint32_t b0, Block4& s1, uint32_t& t1, uint32_t b1,
-                                           uint4 cs, uint32_t cctl) {
-  Block4 h0 = s0, h1 = s1;
-  dpf_aes::mmo_hash2(h0, h1, lk, SelectRK{rkl.k, rkd.k, 0u - b0}, SelectRK{rkl.k, rkd.k, 0u - b1});
-  uint32_t m0 = 0u - t0, m1 = 0u - t1;
-  h0.w0 ^= cs.x & m0; h0.w1 ^= cs.y & m0; h0.w2 ^= cs.z & m0; h0.w3 ^= cs.w & m0;
-  h1.w0 ^= cs.x & m1; h1.w1 ^= cs.y & m1; h1.w2 ^= cs.z & m1; h1.w3 ^= cs.w & m1;
-  uint32_t n0 = (h0.w0 & 1u) ^ (t0 & ((cctl >> b0) & 1u));
-  uint32_t n1 = (h1.w0 & 1u) ^ (t1 & ((cctl >> b1) & 1u));
-  h0.w0 &= ~1u;
-  h1.w0 &= ~1u;
-  s0 = h0; t0 = n0;
-  s1 = h1; t1 = n1;
-}
-
-using u128 = unsigned __int128;
-
-__device__ __forceinline__ u128 block_u128(Block4 h) {
-  return ((u128)h.w3 << 96) | ((u128)h.w2 << 64) | ((u128)h.w1 << 32) | h.w0;
-}
-__device__ __forceinline__ u128 dpf_u128(dpf_block c) { return ((u128)c.high << 64) | c.low; }
-
-// Element `bi` of a directly converted integer block, corrected and negated
-// (distributed_point_function.h:993-1002; value_type_helpers.h:199-211).
-template <int BITS>
-__device__ __forceinline__ u128 fast_point_value(Block4 h, uint32_t t, int bi, u128 cv, int party,
-                                                 int xor_mode) {
-  u128 x = block_u128(h);
-  if (BITS < 128) x >>= (bi * BITS) & 127;
-  if (xor_mode) {
-    if (t) x ^= cv;
-  } else {
-    if (t) x += cv;
-    if (party == 1) x = 0 - x;
-  }
-  if (BITS < 128) x &= (((u128)1 << (BITS & 127)) - 1);
-  return x;
-}
-
-template <int BITS>
-__device__ __forceinline__ void store_bits(char* o, u128 x) {
-  if (BITS == 128) {
-    *reinterpret_cast<uint4*>(o) = make_uint4((uint32_t)x, (uint32_t)(x >> 32),
-                                              (uint32_t)(x >> 64), (uint32_t)(x >> 96));
-  } else if (BITS == 64) {
-    *reinterpret_cast<uint64_t*>(o) = (uint64_t)x;
-  } else if (BITS == 32) {
-    *reinterpret_cast<uint32_t*>(o) = (uint32_t)x;
-  } else if (BITS == 16) {
-    *reinterpret_cast<uint16_t*>(o) = (uint16_t)x;
-  } else {
-    *reinterpret_cast<uint8_t*>(o) = (uint8_t)x;
-  }
-}
-
-// Adds v to a 192-bit little-endian accumulator held in three u64 words.
-// Exact under any interleaving of concurrent adders: each word's carry-out is
-// derived from the value the atomic returned.
-__device__ __forceinline__ void wide_add(unsigned long long* w, u128 v) {
-  unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
-  unsigned long long old = atomicAdd(w, lo);
-  unsigned long long c = (old + lo) < old ? 1ull : 0ull;
-  unsigned long long h = hi + c;
-  unsigned long long c2 = (h < hi) ? 1ull : 0ull;
-  if (h) {
-    unsigned long long old2 = atomicAdd(w + 1, h);
-    c2 += (old2 + h) < old2 ? 1ull : 0ull;
-  }
-  if (c2) atomicAdd(w + 2, c2);
-}
-__device__ __forceinline__ void wide_xor(unsigned long long* w, u128 v) {
-  atomicXor(w, (unsigned long long)v);
-  atomicXor(w + 1, (unsigned long long)(v >> 64));
-}
-
-// Packed-element conversion for the generic path: element `e` of the hashed
-// leaf, corrected and negated, as per-leaf values.
-__device__ void generic_point_values(const GenericLeaf& g, const LdsLookup& lk, const uint32_t* rkv,
-                                     Block4 seed, uint32_t t, int e, const dpf_block* vcw,
-                                     int party, u128* vals) {
-  char buf[16 * DPF_MAX_LEAVES];
-  GenericLeaf lf = g;
-  lf.vcw = vcw;
-  lf.party = party;
-  lf.convert_store(lk, rkv, seed, t, e, 1, buf);
-  int off = 0;
-  for (int k = 0; k < g.d.num_leaves; ++k) {
-    int lb = g.d.bits[k] >> 3;
-    vals[k] = GenericLeaf::load_le(reinterpret_cast<const uint8_t*>(buf) + off, lb);
-    off += lb;
-  }
-}
-
-__device__ __forceinline__ u128 leaf_group_add(const dpf_value_desc& d, int k, u128 a, u128 b) {
-  if (d.kind[k] == DPF_LEAF_XOR) return a ^ b;
-  if (d.kind[k] == DPF_LEAF_INTMODN) {
-    u128 n = ((u128)d.mod_high[k] << 64) | d.mod_low[k], c = n - b;
-    return a >= c ? a - c : n - c + a;
-  }
-  u128 m = d.bits[k] >= 128 ? ~(u128)0 : (((u128)1 << d.bits[k]) - 1);
-  return (a + b) & m;
-}
-
 template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void eval_points_kernel(PointParams p, Leaf leaf) {
   __shared__ LdsImage lds;
@@ -830,40 +316,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   }
 }
 
-// Turns the 192-bit exact per-leaf sums into group elements and packs them:
-// plain integers keep the low `bits`, XorWrapper is already reduced, IntModN
-// takes the sum mod N (int_mod_n.h:116-120).
-__global__ void finalize_sums_kernel(int64_t num_points, dpf_value_desc d,
-                                     const unsigned long long* __restrict__ wide,
-                                     char* __restrict__ out) {
-  const int nl = d.num_leaves;
-  int esz = 0;
-  for (int k = 0; k < nl; ++k) esz += d.bits[k] >> 3;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < num_points;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    char* o = out + i * esz;
-    for (int k = 0; k < nl; ++k) {
-      const unsigned long long* w = wide + (i * nl + k) * 3;
-      u128 v = ((u128)w[1] << 64) | w[0];
-      if (d.kind[k] == DPF_LEAF_INTMODN) {
-        const u128 n = ((u128)d.mod_high[k] << 64) | d.mod_low[k];
-        // r = (w2 * 2^128 + v) mod n, one bit at a time (r < n throughout).
-        u128 r = 0;
-        for (int b = 191; b >= 0; --b) {
-          const unsigned bit = b >= 128 ? (unsigned)((w[2] >> (b - 128)) & 1)
-                                        : (unsigned)((v >> b) & 1);
-          r = (r >= n - r) ? r - (n - r) : r + r;  // 2r mod n
-          if (bit) r = (r >= n - 1) ? 0 : r + 1;   // +1 mod n
-        }
-        v = r;
-      }
-      const int lb = d.bits[k] >> 3;
-      for (int b = 0; b < lb; ++b) { o[b] = (char)(uint8_t)v; v >>= 8; }
-      o += lb;
-    }
-  }
-}
-
 // Counts points >= 2^log_domain_size (EvaluateAt's range check, h:861-874).
 __global__ void count_out_of_range_kernel(int64_t n, const dpf_block* __restrict__ pts, int log,
                                           unsigned long long* __restrict__ bad) {
@@ -916,6 +368,9 @@ __global__ void sum_shares_kernel(int64_t num_keys, int64_t row_len, int bits, i
 // ------------------------------------------------------------------------
 // Host-side launch helpers
 // ------------------------------------------------------------------------
+}  // namespace
+
+namespace dpf_rt {
 int num_cus() {
   static int cus = 0;
   if (cus == 0) {
@@ -964,11 +419,10 @@ bool fast_int(const dpf_value_desc* d) {
          d->kind[0] != DPF_LEAF_INTMODN;
 }
 
-RoundKeys xor_keys(const RoundKeys& a, const RoundKeys& b) {
-  RoundKeys r;
-  for (int i = 0; i < 44; ++i) r.k[i] = a.k[i] ^ b.k[i];
-  return r;
-}
+
+}  // namespace dpf_rt
+
+namespace {
 
 template <class Leaf>
 int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
@@ -1068,7 +522,7 @@ int make_point_params(int64_t num_keys, int64_t points_per_key, int num_levels,
 extern "C" {
 
 int dpf_hip_abi_version(void) { return DPF_HIP_ABI_VERSION; }
-const char* dpf_hip_last_error(void) { return g_last_error.c_str(); }
+const char* dpf_hip_last_error(void) { return dpf_rt::g_last_error.c_str(); }
 
 int dpf_hip_device_count(int* count) {
   HIP_TRY(hipGetDeviceCount(count));

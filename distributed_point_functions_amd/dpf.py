@@ -64,6 +64,11 @@ def _call(fn, *args):
         raise DpfStatusError(int(code), msg) from None
 
 
+def u128_from_block(b) -> int:
+    """Python int of a proto Block {high, low}."""
+    return (int(b.high) << 64) | int(b.low)
+
+
 def u128_array(xs: Sequence[int]) -> np.ndarray:
     a = np.empty((len(xs), 2), dtype=np.uint64)
     for i, x in enumerate(xs):
@@ -373,6 +378,41 @@ class DistributedPointFunction:
         _call(self._impl.evaluate_at_batch_sum_to_device, device_batch, int(hierarchy_level),
               points.data_ptr(), int(points.shape[0]), out.data_ptr(), s.cuda_stream)
 
+    # -- device-resident incremental evaluation of a key batch (8f.1, cfg 5b) --
+    def create_batch_evaluation_context(self, device_batch):
+        """EvaluationContext of every key of a device batch, kept on the GPU."""
+        return _call(self._impl.create_batch_evaluation_context, device_batch)
+
+    def evaluate_until_batch_to_device(self, hierarchy_level: int, prefixes, batch_ctx, out,
+                                       sum_over_keys: bool = False, stream=None) -> int:
+        """EvaluateUntil(hierarchy_level, prefixes, ctx_k) for every key k of the
+        batch (same prefixes for all keys).  Packed outputs go to the torch
+        device tensor `out`: [key][element], or with `sum_over_keys` the group
+        sum over keys [element].  Returns the elements per key."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        pre = prefixes if isinstance(prefixes, np.ndarray) else u128_array(prefixes)
+        return _call(self._impl.evaluate_until_batch_to_device, int(hierarchy_level), pre,
+                     batch_ctx, bool(sum_over_keys), out.data_ptr(),
+                     out.numel() * out.element_size(), s.cuda_stream)
+
+    def evaluate_next_batch_to_device(self, prefixes, batch_ctx, out, sum_over_keys: bool = False,
+                                      stream=None) -> int:
+        """EvaluateNext for every key of the batch (h:363-365)."""
+        level = 0 if len(prefixes) == 0 else batch_ctx.previous_hierarchy_level + 1
+        return self.evaluate_until_batch_to_device(level, prefixes, batch_ctx, out,
+                                                   sum_over_keys, stream)
+
+    def export_evaluation_context(self, batch_ctx, host_batch, k: int,
+                                  stream=None) -> pb.EvaluationContext:
+        """Key k's context as the EvaluationContext proto EvaluateUntil leaves."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        ctx = pb.EvaluationContext()
+        ctx.ParseFromString(_call(self._impl.export_evaluation_context, batch_ctx, host_batch,
+                                  int(k), s.cuda_stream))
+        return ctx
+
     def sum_packed_shares(self, hierarchy_level: int, shares: np.ndarray, num_shares: int,
                           count: int) -> np.ndarray:
         """Group sum of num_shares packed vectors of `count` elements (host)."""
@@ -382,6 +422,11 @@ class DistributedPointFunction:
 
     def packed_size(self, h: int) -> int:
         return self._impl.packed_size(h)
+
+    def output_elements(self, h: int, num_prefixes: int, previous_hierarchy_level: int) -> int:
+        """Elements EvaluateUntil(h, prefixes) returns for len(prefixes) == num_prefixes."""
+        return _call(self._impl.output_elements, int(h), int(num_prefixes),
+                     int(previous_hierarchy_level))
 
     def tree_levels_needed(self) -> int:
         return self._impl.tree_levels_needed()

@@ -243,6 +243,30 @@ class DistributedPointFunction {
   Status EvaluateAtBatchSumToDevice(const DeviceKeyBatch& keys, int hierarchy_level,
                                     const void* device_points, int64_t num_points,
                                     void* device_out, void* stream) const;
+  // ---- device-resident incremental evaluation of a key batch (8f.1, cfg 5b)
+  // A fresh context for every key of `keys` (previous_hierarchy_level -1), as
+  // CreateEvaluationContext would make per key.  `keys` must outlive it.
+  StatusOr<std::unique_ptr<DeviceBatchContext>> CreateBatchEvaluationContext(
+      const DeviceKeyBatch& keys) const;
+  // EvaluateUntil(hierarchy_level, prefixes, ctx_k) for every key k of the
+  // batch, at the same prefixes for all keys (same validation and errors as
+  // EvaluateUntil): writes num_keys rows of n packed elements ([key][element])
+  // to device_out and returns n.
+  StatusOr<int64_t> EvaluateUntilBatchToDevice(int hierarchy_level, Span<const uint128> prefixes,
+                                               DeviceBatchContext& ctx, void* device_out,
+                                               int64_t capacity_bytes, void* stream) const;
+  // Aggregation variant: out[j] = group sum over the batch's keys of
+  // EvaluateUntil(hierarchy_level, prefixes, ctx_k)[j] (n packed elements).
+  StatusOr<int64_t> EvaluateUntilBatchSumToDevice(int hierarchy_level,
+                                                  Span<const uint128> prefixes,
+                                                  DeviceBatchContext& ctx, void* device_out,
+                                                  int64_t capacity_bytes, void* stream) const;
+  // Key k's context as the EvaluationContext proto EvaluateUntil would have
+  // left (lazy serialization; `host_keys` is the batch `ctx` was uploaded from).
+  StatusOr<EvaluationContext> ExportEvaluationContext(const DeviceBatchContext& ctx,
+                                                      const KeyBatch& host_keys, int64_t k,
+                                                      void* stream) const;
+
   // Group sum of `num_shares` packed output vectors of `count` elements each
   // (host memory), e.g. per-GPU partial sums after an all-gather.
   StatusOr<std::vector<uint8_t>> SumPackedShares(int hierarchy_level, const uint8_t* shares,
@@ -303,6 +327,10 @@ class DistributedPointFunction {
                                    DeviceStart* out, void* stream,
                                    const std::function<Status()>& before_device) const;
   StatusOr<std::vector<uint128>> ValueCorrectionLeaves(const DpfKey& key, int h) const;
+  // Shared core of the two batched EvaluateUntil entry points.
+  StatusOr<int64_t> EvaluateUntilBatchCore(int hierarchy_level, Span<const uint128> prefixes,
+                                           DeviceBatchContext& ctx, bool sum, void* device_out,
+                                           int64_t capacity_bytes, void* stream) const;
 
   std::unique_ptr<dpf_internal::ProtoValidator> validator_;
   std::vector<int> blocks_needed_;

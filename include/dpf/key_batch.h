@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "dpf/status.h"
+#include "dpf/uint128.h"
 #include "dpf_hip.h"
 
 namespace distributed_point_functions {
@@ -76,6 +77,66 @@ class DeviceKeyBatch {
   void* cw_left_ = nullptr;
   void* cw_right_ = nullptr;
   std::vector<void*> vcw_;
+};
+
+// The EvaluationContext (distributed_point_function.proto:142-171) of every key
+// of a DeviceKeyBatch, kept in device memory between incremental evaluations
+// (SURVEY.md 8f.1): the batch is evaluated at the SAME prefixes for all keys
+// (the heavy-hitters pattern of config 5b), so the context holds one shared
+// list of partial-evaluation prefixes (tree indices at depth
+// hierarchy_to_tree[partial_evaluations_level]) and, per key, the seed and
+// control bit at each of them -- key-major, [key][prefix] -- instead of a
+// protobuf repeated field per key.  Created by
+// DistributedPointFunction::CreateBatchEvaluationContext; serialized lazily to
+// a per-key EvaluationContext proto by ExportEvaluationContext.
+class DeviceBatchContext {
+ public:
+  DeviceBatchContext(const DeviceBatchContext&) = delete;
+  DeviceBatchContext& operator=(const DeviceBatchContext&) = delete;
+  ~DeviceBatchContext();
+
+  const DeviceKeyBatch& keys() const { return *keys_; }
+  int previous_hierarchy_level() const { return previous_hierarchy_level_; }
+  int partial_evaluations_level() const { return partial_evaluations_level_; }
+  // Shared partial-evaluation prefixes (tree indices), in evaluation order.
+  const std::vector<uint128>& partial_prefixes() const { return partial_prefixes_; }
+  // Device arrays [num_keys][partial_prefixes().size()].
+  const dpf_block* partial_seeds() const { return static_cast<const dpf_block*>(seeds_); }
+  const uint8_t* partial_control() const { return static_cast<const uint8_t*>(ctrl_); }
+  // Back to the state CreateBatchEvaluationContext returns, keeping the device
+  // allocations for the next pass over the hierarchy.
+  void Reset() {
+    previous_hierarchy_level_ = -1;
+    partial_evaluations_level_ = -1;
+    partial_prefixes_.clear();
+  }
+
+ private:
+  friend class DistributedPointFunction;
+  explicit DeviceBatchContext(const DeviceKeyBatch* keys) : keys_(keys) {}
+  // Grows a device allocation (contents are not preserved).
+  static Status Ensure(void** p, size_t* cap, size_t bytes);
+
+  const DeviceKeyBatch* keys_;
+  int previous_hierarchy_level_ = -1;
+  int partial_evaluations_level_ = -1;
+  std::vector<uint128> partial_prefixes_;
+  void* seeds_ = nullptr;  // current partial evaluations
+  void* ctrl_ = nullptr;
+  size_t seeds_cap_ = 0, ctrl_cap_ = 0;
+  void* next_seeds_ = nullptr;  // written by the next evaluation, then swapped in
+  void* next_ctrl_ = nullptr;
+  size_t next_seeds_cap_ = 0, next_ctrl_cap_ = 0;
+  // Per-call scratch: start-node tables, sums workspace, staging output.
+  void* parent_ = nullptr;
+  void* path_ = nullptr;
+  void* save_ = nullptr;
+  void* offsets_ = nullptr;
+  void* workspace_ = nullptr;
+  void* stage_ = nullptr;
+  void* stage2_ = nullptr;
+  size_t parent_cap_ = 0, path_cap_ = 0, save_cap_ = 0, offsets_cap_ = 0, workspace_cap_ = 0,
+         stage_cap_ = 0, stage2_cap_ = 0;
 };
 
 }  // namespace distributed_point_functions

@@ -201,6 +201,64 @@ int dpf_hip_gather(int64_t num_rows, int64_t count, int elem_size, const int64_t
 int dpf_hip_sum_shares_u64(int64_t num_keys, int64_t row_len, int bits, int xor_mode,
                            const void* shares, uint64_t* sums, void* stream);
 
+/* ---- a7+a8+a9+a4+a5+a6 over a key batch at shared prefixes ----------------
+ * One EvaluateUntil step (distributed_point_function.h:641-837) of every key
+ * of a batch with a device-resident context: the
+ * path walk of ComputePartialEvaluations (cc:351-453, EvaluateSeeds
+ * evaluate_prg_hwy.cc:452-486), ExpandSeeds (cc:271-349), HashExpandedSeeds
+ * (cc:500-524) and the value correction (h:785-808), fused.
+ *
+ * For key k < num_keys and start node u < num_starts:
+ *   start  = (seeds_in[k*in_stride + parent[u]], control_in[...]), or key k's
+ *            root (key_seed[k], party[k]) when seeds_in == NULL;
+ *   walk   walk_levels levels along path[u] (bit walk_levels-1-j at step j)
+ *          with key k's correction words cw_first + j (rows of cw_stride);
+ *          after save_after steps (-1 = never) the node is stored at
+ *          seeds_out/control_out[k*out_stride + save_index[u]] when
+ *          save_index[u] >= 0;
+ *   expand expand_levels (<= dpf_hip_prefix_batch_max_expand) full levels
+ *          below it (correction words cw_first + walk_levels + d), hash
+ *          every leaf, convert it and keep its first elements_per_leaf
+ *          corrected elements (value_correction[k*E*num_leaves ...], party
+ *          negation).
+ * Slot (u << expand_levels) + leaf, element e is output element
+ * ((u << expand_levels) + leaf) * elements_per_leaf + e.
+ * sum == 0: out[k][slot] packed, one row of num_starts << expand_levels
+ *           elements per key (== EvaluateUntil's block for that node).
+ * sum != 0: out[slot] = group sum over keys (integers mod 2^bits, IntModN mod
+ *           N, XorWrapper by XOR); workspace holds slots * num_leaves * 3
+ *           uint64 and is cleared by the call.  Returns 12 UNIMPLEMENTED for
+ *           value types without an on-device key sum
+ *           (dpf_hip_prefix_batch_max_expand(desc, 1) < 0): use sum == 0 and
+ *           dpf_hip_sum_rows. */
+int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_levels,
+                              int save_after, int expand_levels, int cw_first, int cw_stride,
+                              const dpf_block* key_seed, const uint8_t* party,
+                              const dpf_block* seeds_in, const uint8_t* control_in,
+                              int64_t in_stride, const int32_t* parent, const dpf_block* path,
+                              const int32_t* save_index, dpf_block* seeds_out,
+                              uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed,
+                              const uint8_t* cw_left, const uint8_t* cw_right,
+                              const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                              const dpf_aes_key* key_value, const dpf_value_desc* desc,
+                              int elements_per_leaf, const dpf_block* value_correction, int sum,
+                              uint64_t* workspace, void* out, void* stream);
+
+/* Largest expand_levels dpf_hip_eval_prefix_batch accepts for this value type
+ * (register-resident subtree), or -1 if `sum` mode is not available. */
+int dpf_hip_prefix_batch_max_expand(const dpf_value_desc* desc, int sum);
+
+/* out[j] = group sum over r < num_rows of in[r*row_len + j], packed elements of
+ * the value type (the generic on-device key sum). */
+int dpf_hip_sum_rows(int64_t num_rows, int64_t row_len, const dpf_value_desc* desc,
+                     const void* in, void* out, void* stream);
+
+/* Per-key gather (h:822-835 for a key batch):
+ * out[k*num_rows*count + i*count + j] = in[k*in_row_elems + src_offset[i] + j]. */
+int dpf_hip_gather_batched(int64_t num_keys, int64_t in_row_elems, int64_t num_rows,
+                           int64_t count, int elem_size, const int64_t* src_offset,
+                           const void* in, void* out, void* stream);
+
 /* ---- timing helpers (hipEvents on the given stream) ------------------------ */
 int dpf_hip_event_create(void** ev);
 int dpf_hip_event_destroy(void* ev);

@@ -7,7 +7,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "distributed_point_functions_amd", "csrc", "kernels", "dpf_kernels.hip")
+SRC = os.path.join(ROOT, "distributed_point_functions_amd", "csrc", "kernels",
+                   os.environ.get("KRES_TU", "dpf_kernels.hip"))
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c",
        f"-I{ROOT}/include", SRC, "-o", "/tmp/_kres.o", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp").stderr
