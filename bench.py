@@ -59,7 +59,8 @@ def parse():
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
     ap.add_argument("--workload", default="full_domain",
                     choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum",
-                             "synthetic_hierarchical", "synthetic_direct", "heavy_hitters"],
+                             "synthetic_hierarchical", "synthetic_hierarchical_device",
+                             "synthetic_direct", "heavy_hitters"],
                     help="full_domain = BASELINE configs[1] (the headline); full_domain_u128 = "
                          "configs[2] (2^31 uint128 outputs per GPU, 2^34 over 8 GPUs); "
                          "evaluate_at(_sum) = configs[3] (2^20 keys x 2^10 points, log 128)")
@@ -480,14 +481,15 @@ def main_synthetic(args):
         raise SystemExit("synthetic_* workloads evaluate one key on one GPU")
     H.load(require_gpu=True)
     mode = "direct" if args.workload == "synthetic_direct" else "hierarchical"
+    device_ctx = args.workload == "synthetic_hierarchical_device"
     conc = 0.0 if args.distribution == "uniform" else float(args.distribution)
     host = D.host()
     # warmup iteration(s) are part of the driver's first call; time a second call.
     for _ in range(max(args.warmup, 0)):
         D._call(host.run_synthetic_data_benchmark, args.domain, 1 << 20, conc, 1, 4, 1,
-                mode == "direct", False)
+                mode == "direct", False, device_ctx)
     r = D._call(host.run_synthetic_data_benchmark, args.domain, 1 << 20, conc, 1, 4,
-                args.steps, mode == "direct", True)
+                args.steps, mode == "direct", True, device_ctx)
     pub = PUBLISHED_SYNTHETIC.get((mode, args.domain), {}).get(args.distribution)
     secs = r["seconds_per_iteration"]
     outs = sum(r["outputs_per_level"])
@@ -501,7 +503,9 @@ def main_synthetic(args):
         "data": "synthetic: 2^20 distinct nonzeros regenerated with the README's distributions "
                 "(the reference CSVs are git-LFS stubs); seed 1",
         "config": {"workload": f"{mode} evaluation of one DpfKey through the DistributedPointFunction "
-                               f"API (EvaluateUntil per level / EvaluateAt), domain 2^{args.domain}",
+                               f"API (EvaluateUntil per level / EvaluateAt), domain 2^{args.domain}" +
+                               (", device-resident context (EvaluateUntilBatchToDevice on a one-key "
+                                "batch, outputs copied to host per level)" if device_ctx else ""),
                    "levels_to_evaluate": r["levels_to_evaluate"],
                    "prefixes_per_level": r["prefixes_per_level"],
                    "outputs_per_level": r["outputs_per_level"],

@@ -389,7 +389,7 @@ PYBIND11_MODULE(_dpf_host, m) {
   });
   m.def("run_synthetic_data_benchmark",
         [](int log, int64_t count, double concentration, uint64_t seed, int mef, int iters,
-           bool only_nonzeros, bool verify) {
+           bool only_nonzeros, bool verify, bool device_context) {
           experiments::BenchmarkOptions o;
           o.log_domain_size = log;
           o.num_nonzeros = count;
@@ -399,6 +399,7 @@ PYBIND11_MODULE(_dpf_host, m) {
           o.num_iterations = iters;
           o.only_nonzeros = only_nonzeros;
           o.verify = verify;
+          o.device_context = device_context;
           experiments::BenchmarkReport r;
           {
             py::gil_scoped_release nogil;
@@ -417,7 +418,10 @@ PYBIND11_MODULE(_dpf_host, m) {
           d["seconds_per_iteration"] = r.seconds_per_iteration;
           d["verified"] = r.verified;
           return d;
-        });
+        },
+        py::arg("log"), py::arg("count"), py::arg("concentration"), py::arg("seed"),
+        py::arg("mef"), py::arg("iters"), py::arg("only_nonzeros"), py::arg("verify"),
+        py::arg("device_context") = false);
   m.def("bits_needed", [](const py::bytes& vt, double sec) {
     return Take(dpf_internal::BitsNeeded(Parse<ValueType>(vt), sec));
   });

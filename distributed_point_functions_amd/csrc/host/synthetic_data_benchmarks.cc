@@ -7,6 +7,8 @@
 #include <random>
 #include <set>
 
+#include "dpf/key_batch.h"
+
 namespace distributed_point_functions {
 namespace experiments {
 
@@ -107,6 +109,58 @@ StatusOr<HierarchicalResult> RunHierarchicalEvaluation(
   return r;
 }
 
+StatusOr<HierarchicalResult> RunHierarchicalEvaluationDeviceContext(
+    const DistributedPointFunction& dpf, const DpfKey& key,
+    const std::vector<std::vector<uint128>>& prefixes_to_evaluate, int num_iterations) {
+  const int H = static_cast<int>(dpf.parameters().size());
+  if (prefixes_to_evaluate.size() != static_cast<size_t>(H))
+    return InvalidArgumentError("one prefix list per hierarchy level expected");
+  const DpfKey* kp = &key;
+  DPF_ASSIGN_OR_RETURN(KeyBatch batch, dpf.MakeKeyBatch(Span<const DpfKey* const>(&kp, 1)));
+  DPF_ASSIGN_OR_RETURN(std::unique_ptr<DeviceKeyBatch> dev, DeviceKeyBatch::Upload(batch, nullptr));
+  DPF_ASSIGN_OR_RETURN(std::unique_ptr<DeviceBatchContext> ctx,
+                       dpf.CreateBatchEvaluationContext(*dev));
+  int64_t max_bytes = 0;
+  for (int level = 0; level < H; ++level) {
+    DPF_ASSIGN_OR_RETURN(int64_t n, dpf.OutputElements(level,
+                                                       static_cast<int64_t>(prefixes_to_evaluate[level].size()),
+                                                       level - 1));
+    max_bytes = std::max(max_bytes, n * 4);
+  }
+  void* out = nullptr;
+  if (int rc = dpf_hip_alloc(&out, std::max<int64_t>(max_bytes, 16)))
+    return Status(static_cast<StatusCode>(rc), dpf_hip_last_error());
+  HierarchicalResult r;
+  Status st = OkStatus();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < num_iterations && st.ok(); ++i) {
+    ctx->Reset();
+    r.outputs_per_level.clear();
+    r.checksum = 0;
+    for (int level = 0; level < H && st.ok(); ++level) {
+      StatusOr<int64_t> n = dpf.EvaluateUntilBatchToDevice(level, prefixes_to_evaluate[level], *ctx,
+                                                           out, max_bytes, nullptr);
+      if (!n.ok()) {
+        st = n.status();
+        break;
+      }
+      // The reference returns the level's outputs in host memory.
+      std::vector<uint32_t> result(*n);
+      if (int rc = dpf_hip_memcpy_d2h(result.data(), out, *n * 4, nullptr)) {
+        st = Status(static_cast<StatusCode>(rc), dpf_hip_last_error());
+        break;
+      }
+      r.outputs_per_level.push_back(*n);
+      r.checksum ^= Fold(result);
+    }
+  }
+  const auto t1 = std::chrono::steady_clock::now();
+  dpf_hip_free(out);
+  DPF_RETURN_IF_ERROR(st);
+  r.seconds_per_iteration = std::chrono::duration<double>(t1 - t0).count() / num_iterations;
+  return r;
+}
+
 StatusOr<HierarchicalResult> RunDirectEvaluation(const DistributedPointFunction& dpf,
                                                  const DpfKey& key,
                                                  const std::vector<uint128>& nonzeros,
@@ -200,6 +254,10 @@ StatusOr<BenchmarkReport> RunSyntheticDataBenchmark(const BenchmarkOptions& o) {
   HierarchicalResult r;
   if (o.only_nonzeros) {
     DPF_ASSIGN_OR_RETURN(r, RunDirectEvaluation(*dpf, keys.first, nonzeros, o.num_iterations));
+  } else if (o.device_context) {
+    DPF_ASSIGN_OR_RETURN(r, RunHierarchicalEvaluationDeviceContext(*dpf, keys.first,
+                                                                   prefixes_to_evaluate,
+                                                                   o.num_iterations));
   } else {
     DPF_ASSIGN_OR_RETURN(r, RunHierarchicalEvaluation(*dpf, keys.first, prefixes_to_evaluate,
                                                       o.num_iterations));
@@ -216,6 +274,13 @@ StatusOr<BenchmarkReport> RunSyntheticDataBenchmark(const BenchmarkOptions& o) {
     } else {
       DPF_RETURN_IF_ERROR(VerifyHierarchicalEvaluation(*dpf, keys.first, keys.second,
                                                        prefixes_to_evaluate, alpha, 1));
+      if (o.device_context) {
+        // The device-context outputs must equal the proto-context API's.
+        DPF_ASSIGN_OR_RETURN(HierarchicalResult api,
+                             RunHierarchicalEvaluation(*dpf, keys.first, prefixes_to_evaluate, 1));
+        if (api.checksum != r.checksum || api.outputs_per_level != r.outputs_per_level)
+          return InternalError("device-context outputs differ from EvaluateUntil's");
+      }
     }
     rep.verified = true;
   }

@@ -47,6 +47,13 @@ StatusOr<HierarchicalResult> RunHierarchicalEvaluation(
     const DistributedPointFunction& dpf, const DpfKey& key,
     const std::vector<std::vector<uint128>>& prefixes_to_evaluate, int num_iterations);
 
+// The same hierarchy through the device-resident context:
+// EvaluateUntilBatchToDevice on a one-key batch, each level's outputs copied
+// to a host vector like the reference returns them.
+StatusOr<HierarchicalResult> RunHierarchicalEvaluationDeviceContext(
+    const DistributedPointFunction& dpf, const DpfKey& key,
+    const std::vector<std::vector<uint128>>& prefixes_to_evaluate, int num_iterations);
+
 // RunBatchedSinglePointEvaluation<uint32_t> (synthetic_data_benchmarks.cc:192-205).
 StatusOr<HierarchicalResult> RunDirectEvaluation(const DistributedPointFunction& dpf,
                                                  const DpfKey& key,
@@ -73,6 +80,7 @@ struct BenchmarkOptions {
   int num_iterations = 3;
   bool only_nonzeros = false;    // direct EvaluateAt instead of the hierarchy
   bool verify = true;            // two-server reconstruction check (untimed)
+  bool device_context = false;   // hierarchical: device-resident context (8f.1)
 };
 struct BenchmarkReport {
   std::vector<int> levels_to_evaluate;
