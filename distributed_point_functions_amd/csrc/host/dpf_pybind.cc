@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "dcf/distributed_comparison_function.h"
 #include "dpf/distributed_point_function.h"
 #include "synthetic_data_benchmarks.h"
 
@@ -326,6 +327,59 @@ class PyDpf {
   std::shared_ptr<DistributedPointFunction> dpf_;
 };
 
+class PyDcf {
+ public:
+  static PyDcf Create(const py::bytes& params) {
+    PyDcf r;
+    r.dcf_ = std::shared_ptr<DistributedComparisonFunction>(
+        Take(DistributedComparisonFunction::Create(Parse<DcfParameters>(params))).release());
+    return r;
+  }
+  py::tuple GenerateKeys(const py::int_& alpha, const py::bytes& beta, const py::object& s0,
+                         const py::object& s1) {
+    std::pair<DcfKey, DcfKey> keys;
+    if (s0.is_none())
+      keys = Take(dcf_->GenerateKeys(IntToU128(alpha), Parse<Value>(beta)));
+    else
+      keys = Take(dcf_->GenerateKeysWithSeeds(IntToU128(alpha), Parse<Value>(beta),
+                                              IntToU128(s0.cast<py::int_>()),
+                                              IntToU128(s1.cast<py::int_>())));
+    return py::make_tuple(Ser(keys.first), Ser(keys.second));
+  }
+  py::array_t<uint8_t> Evaluate(const py::bytes& key,
+                                const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& xs,
+                                const py::object& vt) {
+    auto x = ToU128(xs);
+    auto t = OptType(vt);
+    return ToArray(Take(dcf_->EvaluatePacked(Parse<DcfKey>(key), MakeConstSpan(x), t.get())));
+  }
+  PyKeyBatch MakeKeyBatch(const std::vector<py::bytes>& keys) {
+    std::vector<DcfKey> k;
+    k.reserve(keys.size());
+    for (const auto& b : keys) k.push_back(Parse<DcfKey>(b));
+    std::vector<const DcfKey*> ptrs;
+    for (const auto& x : k) ptrs.push_back(&x);
+    return PyKeyBatch{std::make_shared<KeyBatch>(Take(dcf_->MakeKeyBatch(MakeConstSpan(ptrs))))};
+  }
+  int64_t EvaluateBatchToDevice(const PyDeviceKeyBatch& keys, uintptr_t points, int64_t ppk,
+                                bool shared, uintptr_t out, int64_t capacity, uintptr_t stream) {
+    py::gil_scoped_release nogil;
+    auto r = dcf_->EvaluateBatchToDevice(*keys.d, reinterpret_cast<const void*>(points), ppk, shared,
+                                         reinterpret_cast<void*>(out), capacity,
+                                         reinterpret_cast<void*>(stream));
+    if (!r.ok()) {
+      py::gil_scoped_acquire g;
+      throw StatusError(r.status());
+    }
+    return *r;
+  }
+  int PackedSize() const { return dcf_->dpf().flat_value_type(0).packed_size; }
+  std::vector<int> HierarchyToTree() const { return dcf_->dpf().hierarchy_to_tree(); }
+
+ private:
+  std::shared_ptr<DistributedComparisonFunction> dcf_;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_dpf_host, m) {
@@ -377,6 +431,15 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("packed_size", &PyDpf::PackedSize)
       .def("corrected_elements_per_block", &PyDpf::CorrectedElementsPerBlock)
       .def("output_elements", &PyDpf::OutputElements);
+  py::class_<PyDcf>(m, "DistributedComparisonFunction")
+      .def_static("create", &PyDcf::Create)
+      .def("generate_keys", &PyDcf::GenerateKeys, py::arg("alpha"), py::arg("beta"),
+           py::arg("seed_0") = py::none(), py::arg("seed_1") = py::none())
+      .def("evaluate", &PyDcf::Evaluate)
+      .def("make_key_batch", &PyDcf::MakeKeyBatch)
+      .def("evaluate_batch_to_device", &PyDcf::EvaluateBatchToDevice)
+      .def("packed_size", &PyDcf::PackedSize)
+      .def("hierarchy_to_tree", &PyDcf::HierarchyToTree);
   m.def("synthetic_levels", [](int log, int64_t count, double concentration, uint64_t seed, int mef) {
     auto nz = experiments::MakeSyntheticNonzeros(count, log, concentration, seed);
     auto prefixes = experiments::ComputePrefixes(nz, log);

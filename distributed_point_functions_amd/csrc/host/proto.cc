@@ -9,6 +9,7 @@
 #include <sstream>
 
 #include "dpf/distributed_point_function.pb.h"
+#include "dcf/distributed_comparison_function.pb.h"
 
 namespace distributed_point_functions {
 namespace {
@@ -546,6 +547,52 @@ bool EvaluationContext::operator==(const EvaluationContext& o) const {
          partials_ == o.partials_ && partials_level_ == o.partials_level_;
 }
 
+// ============================================================== DCF messages
+// dcf/distributed_comparison_function.proto: DcfParameters{parameters = 1},
+// DcfKey{key = 1}.
+bool DcfParameters::SerializeToString(std::string* out) const {
+  out->clear();
+  Writer w{out};
+  if (has_params_) w.msg(1, params_);
+  return true;
+}
+bool DcfParameters::ParseFromArray(const void* d, int n) {
+  *this = DcfParameters();
+  return ParseFields(d, n, [&](int f, int wt, Reader& r) {
+    if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_parameters());
+    r.skip(wt);
+    return r.ok;
+  });
+}
+std::string DcfParameters::DebugString() const {
+  Text t;
+  if (has_params_) t.msg("parameters", params_);
+  return t.os.str();
+}
+bool DcfParameters::operator==(const DcfParameters& o) const {
+  return has_params_ == o.has_params_ && params_ == o.params_;
+}
+bool DcfKey::SerializeToString(std::string* out) const {
+  out->clear();
+  Writer w{out};
+  if (has_key_) w.msg(1, key_);
+  return true;
+}
+bool DcfKey::ParseFromArray(const void* d, int n) {
+  *this = DcfKey();
+  return ParseFields(d, n, [&](int f, int wt, Reader& r) {
+    if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_key());
+    r.skip(wt);
+    return r.ok;
+  });
+}
+std::string DcfKey::DebugString() const {
+  Text t;
+  if (has_key_) t.msg("key", key_);
+  return t.os.str();
+}
+bool DcfKey::operator==(const DcfKey& o) const { return has_key_ == o.has_key_ && key_ == o.key_; }
+
 #define DPF_PARSE_FROM_STRING(Name) \
   bool Name::ParseFromString(const std::string& s) { \
     return ParseFromArray(s.data(), static_cast<int>(s.size())); \
@@ -563,5 +610,7 @@ DPF_PARSE_FROM_STRING(CorrectionWord)
 DPF_PARSE_FROM_STRING(DpfKey)
 DPF_PARSE_FROM_STRING(PartialEvaluation)
 DPF_PARSE_FROM_STRING(EvaluationContext)
+DPF_PARSE_FROM_STRING(DcfParameters)
+DPF_PARSE_FROM_STRING(DcfKey)
 
 }  // namespace distributed_point_functions

@@ -90,11 +90,23 @@ def _build():
     _field(ec, "partial_evaluations", 4, M, R, "PartialEvaluation")
     _field(ec, "partial_evaluations_level", 5, _F.TYPE_INT32)
 
+    # dcf/distributed_comparison_function.proto
+    dcf = descriptor_pb2.FileDescriptorProto()
+    dcf.name = "dcf/distributed_comparison_function.proto"
+    dcf.package = _PKG
+    dcf.syntax = "proto3"
+    dcf.dependency.append(fd.name)
+    dp = dcf.message_type.add(name="DcfParameters")
+    _field(dp, "parameters", 1, M, O, "DpfParameters")
+    dk = dcf.message_type.add(name="DcfKey")
+    _field(dk, "key", 1, M, O, "DpfKey")
+
     pool = descriptor_pool.DescriptorPool()
     pool.Add(fd)
+    pool.Add(dcf)
     out = {}
     for name in ("ValueType", "Value", "DpfParameters", "Block", "CorrectionWord", "DpfKey",
-                 "PartialEvaluation", "EvaluationContext"):
+                 "PartialEvaluation", "EvaluationContext", "DcfParameters", "DcfKey"):
         out[name] = message_factory.GetMessageClass(pool.FindMessageTypeByName(f"{_PKG}.{name}"))
     return out
 
@@ -108,3 +120,5 @@ CorrectionWord = _CLASSES["CorrectionWord"]
 DpfKey = _CLASSES["DpfKey"]
 PartialEvaluation = _CLASSES["PartialEvaluation"]
 EvaluationContext = _CLASSES["EvaluationContext"]
+DcfParameters = _CLASSES["DcfParameters"]
+DcfKey = _CLASSES["DcfKey"]

@@ -259,6 +259,28 @@ int dpf_hip_gather_batched(int64_t num_keys, int64_t in_row_elems, int64_t num_r
                            int64_t count, int elem_size, const int64_t* src_offset,
                            const void* in, void* out, void* stream);
 
+/* ---- batched DCF evaluation ------------------------------
+ * DistributedComparisonFunction::Evaluate (dcf/distributed_comparison_function
+ * .h:83-105) for every (key, point) of a key batch of the DCF's incremental
+ * DPF (num_levels = the DCF's log domain size n, level i has log domain i):
+ *   out[k*points_per_key + j] = sum over levels i with bit (n-1-i) of x == 0
+ *                               of EvaluateAt(key_k, i, {x >> (n - i)})
+ * (for n == 128 the reference uses prefix 0 at every level; mirrored), with
+ * x = points[shared_points ? j : k*points_per_key + j] and the sum in the
+ * value type's group.  level_depth / level_blocks (host arrays of n) are
+ * hierarchy_to_tree and blocks_needed; value_correction (host array of n
+ * device pointers) holds level i's value corrections [key][E*num_leaves]. */
+int dpf_hip_dcf_eval_batch(int64_t num_keys, int64_t points_per_key, int shared_points,
+                           int num_levels, const int32_t* level_depth,
+                           const int32_t* level_blocks, const dpf_block* key_seed,
+                           const uint8_t* party, const dpf_block* points,
+                           const dpf_block* cw_seed, const uint8_t* cw_left,
+                           const uint8_t* cw_right, int cw_stride,
+                           const dpf_block* const* value_correction,
+                           const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+                           const dpf_aes_key* key_value, const dpf_value_desc* desc,
+                           void* out, void* stream);
+
 /* ---- timing helpers (hipEvents on the given stream) ------------------------ */
 int dpf_hip_event_create(void** ev);
 int dpf_hip_event_destroy(void* ev);

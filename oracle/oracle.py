@@ -594,3 +594,44 @@ def evaluate_at(P: OracleParams, key, h: int, points: Sequence[int], ctx=None) -
     if ctx is not None:
         ctx["prev"] = h
     return out
+
+
+# --------------------------------------------------------------------------
+# Distributed comparison function (dcf/distributed_comparison_function.{h,cc})
+# --------------------------------------------------------------------------
+
+def dcf_params(n: int, vt, sec: float = 0.0) -> OracleParams:
+    """The DCF's incremental DPF: level i has log domain i (cc:57-63)."""
+    return OracleParams([(i, vt, sec) for i in range(n)])
+
+
+def dcf_zero_like(vt, beta_leaves: Sequence[int]) -> List[int]:
+    """SetToZero (cc:21-32): integer and IntModN leaves (also inside tuples)
+    become 0; XorWrapper values are left unchanged, as in the reference."""
+    return [b if kind == LEAF_XOR else 0 for (kind, _, _), b in zip(leaves(vt), beta_leaves)]
+
+
+def dcf_generate_keys(P: OracleParams, alpha: int, beta_leaves: Sequence[int],
+                      seed0: int, seed1: int):
+    """GenerateKeys (cc:79-101): level i's value is beta if bit (n-1-i) of alpha
+    is set, else SetToZero(beta); the DPF point is alpha >> 1."""
+    n = len(P.log_domain)
+    vt = P.vtypes[0]
+    betas = [list(beta_leaves) if (alpha >> (n - i - 1)) & 1 else dcf_zero_like(vt, beta_leaves)
+             for i in range(n)]
+    return generate_keys(P, alpha >> 1, betas, seed0, seed1)
+
+
+def dcf_evaluate(P: OracleParams, key, x: int) -> np.ndarray:
+    """Evaluate<T> (h:83-105): the sum over levels i with bit (n-1-i) of x clear
+    of EvaluateAt(key, i, {x >> (n - i)}) (prefix 0 when n == 128).  Returns one
+    packed element (1, packed_size)."""
+    n = len(P.log_domain)
+    vt = P.vtypes[0]
+    acc = np.zeros((1, packed_size(vt)), np.uint8)
+    for i in range(n):
+        prefix = x >> (n - i) if n < 128 else 0
+        e = evaluate_at(P, key, i, [prefix])
+        if not (x >> (n - i - 1)) & 1:
+            acc = add_packed(vt, acc, e)
+    return acc
