@@ -40,7 +40,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 LOG_PER_GPU = 30          # 2^30 uint64 outputs per GPU (BASELINE.json configs[1])
-AES_PEAK_GBLOCKS = 122.9  # integer-VALU AES-128 roofline (DESIGN.md "Roofline")
+# AES-128 rooflines (DESIGN.md "Roofline"), 256 CUs at 2.4 GHz:
+#  * LDS: a T-table block needs 160 conflict-free ds_read_b32 lookups = 640 B at
+#    128 B/clk/CU -> 5 clk/block/CU -> 122.9 G blocks/s.  This binds the
+#    T-table design the kernels use, so it is the `roofline` peak.
+#  * VALU: 320 lane-ops/block at 4 SIMD-32 x 32 lanes = 128 lane-ops/clk/CU ->
+#    2.5 clk/block/CU -> 245.8 G blocks/s (reported as `roofline_valu`).
+AES_PEAK_GBLOCKS = 122.9
+AES_VALU_PEAK_GBLOCKS = 245.8
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
 METRIC = "DPF leaf evals/sec, full-domain 2^30 uint64 at 1/2/4/8 GPUs; AES blocks/s"
 KERNEL = "expand_kernel<FastIntLeaf<64, false> >"
@@ -60,7 +67,7 @@ def parse():
     ap.add_argument("--workload", default="full_domain",
                     choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum",
                              "synthetic_hierarchical", "synthetic_hierarchical_device",
-                             "synthetic_direct", "heavy_hitters"],
+                             "synthetic_direct", "heavy_hitters", "dcf"],
                     help="full_domain = BASELINE configs[1] (the headline); full_domain_u128 = "
                          "configs[2] (2^31 uint128 outputs per GPU, 2^34 over 8 GPUs); "
                          "evaluate_at(_sum) = configs[3] (2^20 keys x 2^10 points, log 128)")
@@ -69,6 +76,8 @@ def parse():
     ap.add_argument("--distribution", default="uniform", choices=["0.1", "0.5", "uniform"],
                     help="synthetic_*: 90%% of nonzeros in the first 10%%/50%% of the domain, or uniform")
     ap.add_argument("--points-log", type=int, default=10, help="evaluate_at: log2 points per key")
+    ap.add_argument("--dcf-keys-log", type=int, default=16, help="dcf: log2 keys")
+    ap.add_argument("--dcf-log-domain", type=int, default=64, help="dcf: log2 comparison domain")
     ap.add_argument("--top-k", type=int, default=1024,
                     help="heavy_hitters: candidates kept per level (children = 4 x top-k)")
     args = ap.parse_args()
@@ -141,7 +150,8 @@ def profiled_traffic(leaves_per_launch: int):
             s = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if s.get("leaves_per_launch") == leaves_per_launch and "hbm_traffic_bytes" in s:
+        if (s.get("leaves_per_launch") == leaves_per_launch and "hbm_traffic_bytes" in s
+                and "expand_kernel" in s.get("kernel", "")):
             best = (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT))
     return best
 
@@ -154,6 +164,8 @@ def main():
         return main_synthetic(args)
     if args.workload == "heavy_hitters":
         return main_heavy_hitters(args)
+    if args.workload == "dcf":
+        return main_dcf(args)
     if args.workload == "full_domain_u128" and args.log_domain == LOG_PER_GPU:
         args.log_domain = 31
     import torch
@@ -252,13 +264,16 @@ def main():
                        "outputs_per_gpu": outputs_per_rank, "tree_levels_per_gpu": depth,
                        "parallelism": f"subtree-prefix x{world}"},
             "aes_blocks_per_s": aes_per_launch * world * args.steps / elapsed,
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
+            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
                          "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
                          "traffic": tr[0] if tr else None,
                          "traffic_source": tr[1] if tr else None,
                          "kernel": KERNEL.replace("64", str(bits)), "launch_ms": kern_ms_max,
                          "algorithmic_aes_per_launch": aes_per_launch,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
+            "roofline_valu": {"bound": "valu", "achieved": achieved,
+                              "peak": AES_VALU_PEAK_GBLOCKS, "unit": "G AES-128 blocks/s",
+                              "frac": achieved / AES_VALU_PEAK_GBLOCKS},
             "roofline_hbm": {"bound": "hbm",
                              "achieved": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -436,7 +451,7 @@ def main_evaluate_at(args):
                        "parallelism": f"key-batch x{world}"},
             "aes_blocks_per_s": n_keys * ppk * (depth + 1) * args.steps / elapsed,
             "keygen_s_rank0": keygen_s, "keygen_threads": threads,
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
+            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
                          "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
                          "traffic": None,
                          "kernel": "eval_points_kernel<GenericLeaf, 64, true, true, %s>" %
@@ -629,7 +644,7 @@ def main_heavy_hitters(args):
             "keygen_s_rank0": keygen_s, "keygen_threads": threads,
             "verified": "two-server reconstruction == plaintext prefix histogram at every level",
             "true_top_k_recall": len(true_top & set(final)) / max(len(true_top), 1),
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
+            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
                          "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
                          "traffic": None, "kernel": "batch_level_kernel<Mod32V, 2, true>",
                          "launch_ms_per_pass": kern_ms_max,
@@ -638,6 +653,133 @@ def main_heavy_hitters(args):
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_heavy_hitters(logs, record, alphas, seeds,
                                                              args.top_k)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+DCF_METRIC = "batched DCF evals/sec (DistributedComparisonFunction::Evaluate), uint64, log domain 64"
+
+
+def main_dcf(args):
+    """SURVEY.md 8f.3: DistributedComparisonFunction::Evaluate for K keys x
+    2^points_log independent points each (uint64, log domain 64), keys split
+    across ranks, outputs [key][point] in HBM.  One fused walk per (key, x)."""
+    import torch
+    import torch.distributed as dist
+    from distributed_point_functions_amd import dcf as C
+    from distributed_point_functions_amd import dpf as D
+    from distributed_point_functions_amd import hip_abi as H
+    from distributed_point_functions_amd import proto as pb
+    from distributed_point_functions_amd import sharding as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    H.load(require_gpu=True)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    n = args.dcf_log_domain
+    params = pb.DcfParameters()
+    params.parameters.log_domain_size = n
+    params.parameters.value_type.CopyFrom(D.integer_type(64))
+    dcf = C.DistributedComparisonFunction.create(params)
+    n_keys, ppk = 1 << args.dcf_keys_log, 1 << args.points_log
+    lo, hi = S.key_range(n_keys, world, rank)
+    rng = np.random.default_rng(0xDCF)
+    alphas = rng.integers(0, 2**63, size=n_keys, dtype=np.uint64)
+    t0 = time.perf_counter()
+    keys = [dcf.generate_keys(int(alphas[k]), 1, seed_0=2 * k + 1, seed_1=2 * k + 2)[0]
+            for k in range(lo, hi)]
+    keygen_s = time.perf_counter() - t0
+    batch = dcf.make_key_batch(keys)
+    dbatch = dcf.upload_key_batch(batch, stream=stream)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99 + rank)
+    nk = hi - lo
+    pts = torch.randint(0, 2**63 - 1, (nk * ppk, 2), dtype=torch.int64, device=dev, generator=gen)
+    if n <= 64:
+        pts[:, 1] = 0
+        if n < 64:
+            pts[:, 0] &= (1 << n) - 1
+    out = torch.empty(nk * ppk * 8, dtype=torch.uint8, device=dev)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record(stream)
+        dcf.evaluate_batch_to_device(dbatch, pts, ppk, out, stream=stream)
+        if evs is not None:
+            evs[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(H.Event(), H.Event()) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
+    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+    # Spot check against the single-key API (itself parity-tested vs the oracle).
+    host_pts = pts.cpu().numpy().view(np.uint64)
+    for k in (0, nk - 1):
+        xs = [int(a) | int(b) << 64 for a, b in host_pts[k * ppk:k * ppk + 16]]
+        want = dcf.evaluate_packed(keys[k], xs).view(np.uint64).reshape(-1)
+        got = out.view(torch.int64)[k * ppk:k * ppk + 16].cpu().numpy().view(np.uint64)
+        if not np.array_equal(got, want):
+            raise SystemExit(f"rank {rank}: DCF batch output of key {lo + k} disagrees")
+    h2t = dcf._impl.hierarchy_to_tree()
+    aes_per_eval = h2t[-1] + (h2t[-1] + 1)      # walk + one value hash per depth
+    aes_launch = nk * ppk * aes_per_eval
+    achieved = aes_launch / (kern_ms_max * 1e-3) / 1e9
+    if rank == 0:
+        res = {
+            "metric": DCF_METRIC, "value": n_keys * ppk * args.steps / elapsed, "unit": "evals/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic: DCF keys from the product keygen (seeded), beta = 1, "
+                    "uniform random points",
+            "config": {"workload": f"DCF Evaluate, {n_keys} keys x {ppk} points, log domain {n}, "
+                                   "uint64", "keys": n_keys, "points_per_key": ppk,
+                       "log_domain_size": n, "parallelism": f"key-batch x{world}"},
+            "aes_blocks_per_s": n_keys * ppk * aes_per_eval * args.steps / elapsed,
+            "keygen_s_rank0": keygen_s,
+            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
+                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
+                         "traffic": None, "kernel": "dcf_eval_kernel<64, true>",
+                         "launch_ms": kern_ms_max, "algorithmic_aes_per_launch": aes_launch},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+            P = O.dcf_params(n, ("int", 64))
+            done, dt = 0, 0.0
+            while dt < 10.0 and done < nk:
+                ok = O.dcf_generate_keys(P, int(alphas[lo + done]), [1], 2 * done + 1,
+                                         2 * done + 2)[0]
+                xs = [int(a) | int(b) << 64 for a, b in host_pts[done * ppk:done * ppk + 64]]
+                t0 = time.perf_counter()
+                for x in xs:
+                    O.dcf_evaluate(P, ok, x)
+                dt += time.perf_counter() - t0
+                done += 1
+            res["cpu_baseline"] = {
+                "value": done * 64 / dt, "unit": "evals/s", "cores": 1, "kind": "port",
+                "sample": f"{done} keys x 64 points: the reference's Evaluate (one EvaluateAt "
+                          f"per level, h:83-105) on the oracle, {dt:.1f} s on 1 host thread"}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
