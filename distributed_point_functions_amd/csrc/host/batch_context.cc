@@ -157,12 +157,18 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         for (size_t j = 0; j < q.size(); ++j) pos.emplace(q[j], static_cast<int32_t>(j));
       }
       parent_of.resize(tree_indices.size());
+      size_t cursor = 0;  // merge pointer while the lookups ascend too
       for (size_t i = 0; i < tree_indices.size(); ++i) {
         const uint128 want = shift < 128 ? tree_indices[i] >> shift : 0;
         int64_t j = -1;
         if (sorted) {
-          auto it = std::lower_bound(q.begin(), q.end(), want);
-          if (it != q.end() && *it == want) j = it - q.begin();
+          if (cursor >= q.size() || q[cursor] > want) cursor = 0;  // lookups went down
+          if (cursor < q.size() && want - q[cursor] < 64) {
+            while (cursor < q.size() && q[cursor] < want) ++cursor;
+          } else {
+            cursor = std::lower_bound(q.begin() + cursor, q.end(), want) - q.begin();
+          }
+          if (cursor < q.size() && q[cursor] == want) j = static_cast<int64_t>(cursor);
         } else {
           auto it = pos.find(want);
           if (it != pos.end()) j = it->second;

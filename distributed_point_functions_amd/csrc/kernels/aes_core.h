@@ -22,6 +22,14 @@
 #define DPF_HD inline
 #endif
 
+// Rounds 1-9 stay a loop by default (code size); -DDPF_AES_UNROLL_ROUNDS
+// unrolls them for scheduling experiments (tools/variant_bench.py).
+#if defined(DPF_AES_UNROLL_ROUNDS)
+#define DPF_ROUND_LOOP _Pragma("unroll")
+#else
+#define DPF_ROUND_LOOP _Pragma("unroll 1")
+#endif
+
 namespace dpf_aes {
 
 // FIPS-197 S-box.
@@ -84,7 +92,7 @@ template <class LK, class RK>
 DPF_HD Block4 encrypt(Block4 s, const LK& lk, const RK& rk) {
   uint32_t w0 = s.w0 ^ rk(0), w1 = s.w1 ^ rk(1), w2 = s.w2 ^ rk(2), w3 = s.w3 ^ rk(3);
 #if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll 1
+  DPF_ROUND_LOOP
 #endif
   for (int r = 1; r < 10; ++r) {
     uint32_t n0 = lk.xor3(lk.template lookup<0, 0>(w0), lk.template lookup<1, 1>(w1),
@@ -133,7 +141,7 @@ DPF_HD void encrypt2(Block4& sa, Block4& sb, const LK& lk, const RKA& ra, const 
   uint32_t a0 = sa.w0 ^ ra(0), a1 = sa.w1 ^ ra(1), a2 = sa.w2 ^ ra(2), a3 = sa.w3 ^ ra(3);
   uint32_t b0 = sb.w0 ^ rb(0), b1 = sb.w1 ^ rb(1), b2 = sb.w2 ^ rb(2), b3 = sb.w3 ^ rb(3);
 #if defined(__HIP_DEVICE_COMPILE__)
-#pragma unroll 1
+  DPF_ROUND_LOOP
 #endif
   for (int r = 1; r < 10; ++r) {
     uint32_t n0 = lk.xor3(lk.template lookup<0, 0>(a0), lk.template lookup<1, 1>(a1),
