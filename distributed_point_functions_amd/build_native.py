@@ -33,6 +33,9 @@ HIP_FLAGS = [
     # reads in flight per wave instead of 2-3 (tools/variant_bench.py, r04:
     # batched points 76 -> 89 G AES/s, expand 82 -> 84).
     "-mllvm", "-amdgpu-sched-strategy=iterative-ilp",
+    # Full-domain expansion finishes each subtree in leaf quads (the last 8 AES
+    # of every 10 as ILP4): expand 87.5 -> 89.2 G AES/s (tools/variant_bench.py, r05).
+    "-DDPF_LEAF_QUADS",
 ]
 
 # Translation units built with LLVM's default scheduler: with iterative-ilp,

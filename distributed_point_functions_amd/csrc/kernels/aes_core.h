@@ -24,6 +24,11 @@
 
 // Rounds 1-9 stay a loop by default (code size); -DDPF_AES_UNROLL_ROUNDS
 // unrolls them for scheduling experiments (tools/variant_bench.py).
+#if defined(__HIPCC__)
+#define DPF_UNROLL _Pragma("unroll")
+#else
+#define DPF_UNROLL
+#endif
 #if defined(DPF_AES_UNROLL_ROUNDS)
 #define DPF_ROUND_LOOP _Pragma("unroll")
 #else
@@ -192,6 +197,68 @@ DPF_HD void mmo_hash2(Block4& xa, Block4& xb, const LK& lk, const RKA& ra, const
   encrypt2(ea, eb, lk, ra, rb);
   xa = Block4{ea.w0 ^ sa.w0, ea.w1 ^ sa.w1, ea.w2 ^ sa.w2, ea.w3 ^ sa.w3};
   xb = Block4{eb.w0 ^ sb.w0, eb.w1 ^ sb.w1, eb.w2 ^ sb.w2, eb.w3 ^ sb.w3};
+}
+
+// N independent encryptions interleaved round by round (ILP N): rk[i]
+// provides chain i's round keys.
+template <int N, class LK, class RK>
+DPF_HD void encryptN(Block4* st, const LK& lk, const RK* rk) {
+  uint32_t w[N][4];
+DPF_UNROLL
+  for (int i = 0; i < N; ++i) {
+    w[i][0] = st[i].w0 ^ rk[i](0);
+    w[i][1] = st[i].w1 ^ rk[i](1);
+    w[i][2] = st[i].w2 ^ rk[i](2);
+    w[i][3] = st[i].w3 ^ rk[i](3);
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  DPF_ROUND_LOOP
+#endif
+  for (int r = 1; r < 10; ++r) {
+    uint32_t n[N][4];
+DPF_UNROLL
+    for (int i = 0; i < N; ++i) {
+DPF_UNROLL
+      for (int c = 0; c < 4; ++c)
+        n[i][c] = lk.xor3(lk.template lookup<0, 0>(w[i][c]), lk.template lookup<1, 1>(w[i][(c + 1) & 3]),
+                          lk.template lookup<2, 2>(w[i][(c + 2) & 3]));
+    }
+DPF_UNROLL
+    for (int i = 0; i < N; ++i) {
+DPF_UNROLL
+      for (int c = 0; c < 4; ++c)
+        n[i][c] = lk.xor3(n[i][c], lk.template lookup<3, 3>(w[i][(c + 3) & 3]), rk[i](4 * r + c));
+    }
+DPF_UNROLL
+    for (int i = 0; i < N; ++i)
+DPF_UNROLL
+      for (int c = 0; c < 4; ++c) w[i][c] = n[i][c];
+  }
+  auto last = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t k) {
+    uint32_t x = lk.template lookup<2, 0>(a), y = lk.template lookup<3, 1>(b);
+    uint32_t z = lk.template lookup<0, 2>(c), u = lk.template lookup<1, 3>(d);
+    uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
+    uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
+    return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ k;
+  };
+DPF_UNROLL
+  for (int i = 0; i < N; ++i)
+    st[i] = Block4{last(w[i][0], w[i][1], w[i][2], w[i][3], rk[i](40)),
+                   last(w[i][1], w[i][2], w[i][3], w[i][0], rk[i](41)),
+                   last(w[i][2], w[i][3], w[i][0], w[i][1], rk[i](42)),
+                   last(w[i][3], w[i][0], w[i][1], w[i][2], rk[i](43))};
+}
+
+// N MMO hashes interleaved.
+template <int N, class LK, class RK>
+DPF_HD void mmo_hashN(Block4* x, const LK& lk, const RK* rk) {
+  Block4 s[N], e[N];
+DPF_UNROLL
+  for (int i = 0; i < N; ++i) e[i] = s[i] = sigma(x[i]);
+  encryptN<N>(e, lk, rk);
+DPF_UNROLL
+  for (int i = 0; i < N; ++i)
+    x[i] = Block4{e[i].w0 ^ s[i].w0, e[i].w1 ^ s[i].w1, e[i].w2 ^ s[i].w2, e[i].w3 ^ s[i].w3};
 }
 
 // Host-side lookup over four plain 256-entry tables (unit checks only).

@@ -45,8 +45,16 @@ RoundKeys expand_key(const dpf_aes_key* key) {
 constexpr int kBlock = 1024;             // threads per workgroup (16 waves)
 constexpr int kTabWords = 4 * 256 * 32;  // 4 tables x 256 entries x 32 bank copies = 128 KiB
 constexpr int kMaxCwLevels = 128;
+#if defined(DPF_LEAF_QUADS)
+#ifndef DPF_QUAD_SMAX
+#define DPF_QUAD_SMAX 11
+#endif
+constexpr int kSMax = DPF_QUAD_SMAX;     // max subtree depth handled per thread
+constexpr int kGMax = kSMax - 2;         // max depth of the DFS stack above leaf quads
+#else
 constexpr int kSMax = 12;                // max subtree depth handled per thread
 constexpr int kGMax = kSMax - 1;         // max depth of the DFS stack above leaf pairs
+#endif
 constexpr int kBMax = 8;                 // max AES blocks hashed per leaf (generic path)
 
 // LDS image: [tables 128 KiB][cw seeds 128 x 16 B][cw control 128 x 4 B]
@@ -293,6 +301,22 @@ struct FastIntLeaf {
       store(s1, leaf + 1, out);
     }
   }
+  // Four consecutive leaves, hashed as one interleaved quadruple.
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+                                        const uint32_t* t, int64_t leaf, char* out) const {
+    const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
+    dpf_aes::mmo_hashN<4>(s, lk, rk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = correct(s[i], t[i]);
+    if (store_bytes == 16) {
+      uint4* p = reinterpret_cast<uint4*>(out + leaf * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) p[i] = make_uint4(s[i].w0, s[i].w1, s[i].w2, s[i].w3);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) store(s[i], leaf + i, out);
+    }
+  }
 };
 
 // Descriptor-driven conversion for Tuple / IntModN / multi-block types
@@ -411,6 +435,10 @@ struct GenericLeaf {
                                         char* out) const {
     emit(lk, rkv, s0, t0, leaf, out);
     emit(lk, rkv, s1, t1, leaf + 1, out);
+  }
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+                                        const uint32_t* t, int64_t leaf, char* out) const {
+    for (int i = 0; i < 4; ++i) emit(lk, rkv, s[i], t[i], leaf + i, out);
   }
 };
 

@@ -122,7 +122,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
   __syncthreads();
   const LdsLookup lk = make_lookup(lds);
   const int k0 = p.k0, S = p.S;
+#if defined(DPF_LEAF_QUADS)
+  // Bottom two levels as quads: a grandparent's two children, their four
+  // children and the four value hashes, the last eight AES as ILP4.
+  const int B = S >= 2 ? 2 : (S >= 1 ? 1 : 0);
+#else
   const int B = S >= 1 ? 1 : 0;  // leaf pairs share their parent
+#endif
   const int G = S - B;            // depth of the DFS stack
   const int64_t ngroups = (int64_t)1 << G;
   for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
     //    children at once (two interleaved hashes); the left child is descended
     //    into and the right one parked in sib[d] until the walk returns to it,
     //    so each node is hashed exactly once and always in a pair.
-    Block4 sib[kGMax + 1];
+    Block4 sib[kGMax];  // sib[d - 1] = parked right child at depth d
     uint32_t tb = 0;  // bit d = control bit of sib[d]
     const int64_t leaf_base = item << S;
     for (int64_t g = 0; g < ngroups; ++g) {
@@ -150,7 +156,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
         ds = G - (int)__builtin_ctzll((unsigned long long)g);
 #pragma unroll
         for (int d = 1; d <= kGMax; ++d)
-          if (d == ds) { node = sib[d]; nt = (tb >> d) & 1u; }
+          if (d == ds) { node = sib[d - 1]; nt = (tb >> d) & 1u; }
       }
       for (int d = ds; d < G; ++d) {
         Block4 c0, c1;
@@ -159,13 +165,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
                       c0, t0, c1, t1);
 #pragma unroll
         for (int e = 1; e <= kGMax; ++e)
-          if (e == d + 1) sib[e] = c1;
+          if (e == d + 1) sib[e - 1] = c1;
         tb = (tb & ~(1u << (d + 1))) | (t1 << (d + 1));
         node = c0;
         nt = t0;
       }
       if (B == 0) {
         leaf.emit(lk, p.rkv.k, node, nt, leaf_base + g, p.out);
+#if defined(DPF_LEAF_QUADS)
+      } else if (B == 2) {
+        const int lvl = k0 + G;
+        Block4 q[4];
+        uint32_t qt[4];
+        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], q[0],
+                      qt[0], q[2], qt[2]);
+        q[1] = q[0];
+        q[3] = q[2];
+        {
+          const UniformRK rk[4] = {UniformRK{p.rkl.k}, UniformRK{p.rkr.k}, UniformRK{p.rkl.k},
+                                   UniformRK{p.rkr.k}};
+          dpf_aes::mmo_hashN<4>(q, lk, rk);
+          const uint4 cs = lds.cw_seed[lvl + 1];
+          const uint32_t cctl = lds.cw_ctrl[lvl + 1];
+          const uint32_t par[4] = {qt[0], qt[0], qt[2], qt[2]};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t m = 0u - par[i];
+            q[i].w0 ^= cs.x & m; q[i].w1 ^= cs.y & m; q[i].w2 ^= cs.z & m; q[i].w3 ^= cs.w & m;
+            qt[i] = (q[i].w0 & 1u) ^ (par[i] & ((cctl >> (i & 1)) & 1u));
+            q[i].w0 &= ~1u;
+          }
+        }
+        leaf.emit4(lk, p.rkv.k, q, qt, leaf_base + 4 * g, p.out);
+#endif
       } else {
         const int lvl = k0 + G;
         Block4 c0, c1;
