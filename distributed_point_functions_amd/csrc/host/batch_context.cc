@@ -17,6 +17,10 @@
 // The host does O(#prefixes) bookkeeping per call; every per-key step runs in
 // one dpf_hip_eval_prefix_batch launch (csrc/kernels/dpf_batch.hip).
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 
 #include "dpf/distributed_point_function.h"
@@ -36,6 +40,32 @@ using dpf_internal::MakeDesc;
 using dpf_internal::SetProtoBlock;
 using dpf_internal::ToBlock;
 using dpf_internal::U128Hash;
+
+namespace {
+// Host-phase timing of the batched path, printed at exit when
+// DPF_BATCH_HOST_TIMING is set (diagnostics for config 5a's host-bound levels).
+struct HostTiming {
+  double t[6] = {0, 0, 0, 0, 0, 0};
+  long calls = 0;
+  ~HostTiming() {
+    if (calls && std::getenv("DPF_BATCH_HOST_TIMING"))
+      std::fprintf(stderr,
+                   "[batch host timing] calls=%ld dedup=%.3fs lookup=%.3fs tables=%.3fs "
+                   "upload=%.3fs device=%.3fs update=%.3fs\n",
+                   calls, t[0], t[1], t[2], t[3], t[4], t[5]);
+  }
+};
+HostTiming g_timing;
+const bool g_timing_on = std::getenv("DPF_BATCH_HOST_TIMING") != nullptr;
+struct PhaseClock {
+  std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+  void mark(int phase) {
+    auto now = std::chrono::steady_clock::now();
+    g_timing.t[phase] += std::chrono::duration<double>(now - last).count();
+    last = now;
+  }
+};
+}  // namespace
 
 Status DeviceBatchContext::Ensure(void** p, size_t* cap, size_t bytes) {
   if (*p && *cap >= bytes) return OkStatus();
@@ -97,43 +127,87 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   int prev_log = 0;
   if (!prefixes.empty()) {
     prev_log = parameters()[prev].log_domain_size();
-    for (uint128 prefix : prefixes)
-      if (prev_log < 128 && prefix >= (static_cast<uint128>(1) << prev_log))
-        return InvalidArgumentError("Index " + Uint128ToString(prefix) +
+    if (prev_log < 128) {
+      const uint128 limit = static_cast<uint128>(1) << prev_log;
+      const int64_t np = static_cast<int64_t>(prefixes.size());
+      std::atomic<int64_t> bad{np};
+      dpf_internal::ParallelFor(np, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i)
+          if (prefixes[i] >= limit) {
+            int64_t cur = bad.load();
+            while (i < cur && !bad.compare_exchange_weak(cur, i)) {
+            }
+            return;
+          }
+      });
+      if (bad.load() < np)
+        return InvalidArgumentError("Index " + Uint128ToString(prefixes[bad.load()]) +
                                     " out of range for hierarchy level " + std::to_string(prev));
+    }
   }
   const int log = parameters()[hierarchy_level].log_domain_size();
   if (log - prev_log > 62)
     return InvalidArgumentError(
         "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
 
+  PhaseClock clk;
+  ++g_timing.calls;
   // Unique tree indices in first-seen order and each prefix's (tree index,
   // block index) (h:718-742).
   const int64_t P = static_cast<int64_t>(prefixes.size());
-  std::vector<uint128> tree_indices;
-  std::vector<std::pair<int64_t, int>> prefix_map;
+  // Host buffers are recycled across calls: first touches of fresh pages cost
+  // more than the bookkeeping itself at 1 M prefixes per level (config 5a).
+  std::vector<uint128> tree_indices = std::move(ctx.spare_prefixes_);
+  tree_indices.clear();
+  static thread_local std::vector<std::pair<int64_t, int>> tl_prefix_map;
+  std::vector<std::pair<int64_t, int>>& prefix_map = tl_prefix_map;
+  prefix_map.clear();
   if (P > 0) {
     const int bib = prev_log - hierarchy_to_tree()[prev];
     tree_indices.reserve(P);
     prefix_map.reserve(P);
-    std::unordered_map<uint128, int64_t, U128Hash> inverse;
-    bool ascending = true;
-    for (int64_t i = 1; i < P && ascending; ++i) ascending = prefixes[i - 1] < prefixes[i];
-    if (!ascending) inverse.reserve(P * 2);
-    for (int64_t i = 0; i < P; ++i) {
-      const uint128 ti = prefixes[i] >> bib;
-      const int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
-      if (ascending) {
-        if (tree_indices.empty() || tree_indices.back() != ti) tree_indices.push_back(ti);
-        prefix_map.emplace_back(static_cast<int64_t>(tree_indices.size()) - 1, bi);
-      } else {
+    const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
+    const int chunks = dpf_internal::NumChunks(P);
+    std::vector<char> chunk_ascending(chunks, 1);
+    dpf_internal::ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
+      for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
+        if (!(prefixes[i - 1] < prefixes[i])) { chunk_ascending[c] = 0; return; }
+    });
+    const bool ascending =
+        std::all_of(chunk_ascending.begin(), chunk_ascending.end(), [](char a) { return a != 0; });
+    if (ascending) {
+      // Equal tree indices are adjacent: a new one starts wherever the tree
+      // index changes.  Two parallel passes: count per chunk, then place.
+      std::vector<int64_t> first(chunks + 1, 0);
+      auto starts = [&](int64_t i) { return i == 0 || (prefixes[i] >> bib) != (prefixes[i - 1] >> bib); };
+      dpf_internal::ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
+        int64_t k = 0;
+        for (int64_t i = lo; i < hi; ++i) k += starts(i);
+        first[c + 1] = k;
+      });
+      for (int c = 0; c < chunks; ++c) first[c + 1] += first[c];
+      tree_indices.resize(first[chunks]);
+      prefix_map.resize(P);
+      dpf_internal::ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
+        int64_t pos = first[c] - 1;
+        for (int64_t i = lo; i < hi; ++i) {
+          if (starts(i)) tree_indices[++pos] = prefixes[i] >> bib;
+          prefix_map[i] = {pos, static_cast<int>(prefixes[i] & bmask)};
+        }
+      });
+    } else {
+      std::unordered_map<uint128, int64_t, U128Hash> inverse;
+      inverse.reserve(P * 2);
+      for (int64_t i = 0; i < P; ++i) {
+        const uint128 ti = prefixes[i] >> bib;
         auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
         if (inserted) tree_indices.push_back(ti);
-        prefix_map.emplace_back(it->second, bi);
+        prefix_map.emplace_back(it->second, static_cast<int>(prefixes[i] & bmask));
       }
     }
   }
 
+  clk.mark(0);
   // Where each tree index starts: a stored partial evaluation or the root
   // (ExpandAndUpdateContext cc:455-498, ComputePartialEvaluations cc:351-453).
   const int Dh = hierarchy_to_tree()[hierarchy_level];
@@ -157,28 +231,41 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         for (size_t j = 0; j < q.size(); ++j) pos.emplace(q[j], static_cast<int32_t>(j));
       }
       parent_of.resize(tree_indices.size());
-      size_t cursor = 0;  // merge pointer while the lookups ascend too
-      for (size_t i = 0; i < tree_indices.size(); ++i) {
-        const uint128 want = shift < 128 ? tree_indices[i] >> shift : 0;
-        int64_t j = -1;
-        if (sorted) {
-          if (cursor >= q.size() || q[cursor] > want) cursor = 0;  // lookups went down
-          if (cursor < q.size() && want - q[cursor] < 64) {
-            while (cursor < q.size() && q[cursor] < want) ++cursor;
+      const int64_t nt = static_cast<int64_t>(tree_indices.size());
+      std::atomic<int64_t> first_missing{nt};
+      dpf_internal::ParallelFor(nt, [&](int64_t lo, int64_t hi) {
+        size_t cursor = 0;  // merge pointer while the lookups ascend too
+        bool fresh = true;
+        for (int64_t i = lo; i < hi; ++i) {
+          const uint128 want = shift < 128 ? tree_indices[i] >> shift : 0;
+          int64_t j = -1;
+          if (sorted) {
+            if (fresh || cursor >= q.size() || q[cursor] > want) {
+              cursor = std::lower_bound(q.begin(), q.end(), want) - q.begin();
+              fresh = false;
+            } else if (want - q[cursor] < 64) {
+              while (cursor < q.size() && q[cursor] < want) ++cursor;
+            } else {
+              cursor = std::lower_bound(q.begin() + cursor, q.end(), want) - q.begin();
+            }
+            if (cursor < q.size() && q[cursor] == want) j = static_cast<int64_t>(cursor);
           } else {
-            cursor = std::lower_bound(q.begin() + cursor, q.end(), want) - q.begin();
+            auto it = pos.find(want);
+            if (it != pos.end()) j = it->second;
           }
-          if (cursor < q.size() && q[cursor] == want) j = static_cast<int64_t>(cursor);
-        } else {
-          auto it = pos.find(want);
-          if (it != pos.end()) j = it->second;
+          if (j < 0) {
+            int64_t cur = first_missing.load();
+            while (i < cur && !first_missing.compare_exchange_weak(cur, i)) {
+            }
+            return;
+          }
+          parent_of[i] = static_cast<int32_t>(j);
         }
-        if (j < 0)
-          return InvalidArgumentError(
-              "Prefix not present in ctx.partial_evaluations at hierarchy level " +
-              std::to_string(prev));
-        parent_of[i] = static_cast<int32_t>(j);
-      }
+      });
+      if (first_missing.load() < nt)
+        return InvalidArgumentError(
+            "Prefix not present in ctx.partial_evaluations at hierarchy level " +
+            std::to_string(prev));
     }
   }
   const int64_t T = static_cast<int64_t>(tree_indices.size());
@@ -211,19 +298,34 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   if (!device_out || capacity_bytes < need) return InvalidArgumentError("device output buffer too small");
   const bool update_ctx = P > 0 && hierarchy_level < H - 1;
 
-  // Start-node tables: u = tree index i * 2^s + sub.
-  std::vector<int32_t> parent(U, 0), save(U, -1);
-  std::vector<dpf_block> path(U);
-  const uint128 w1_mask = W1 >= 128 ? ~uint128{0} : ((uint128{1} << W1) - 1);
-  for (int64_t i = 0; i < T; ++i) {
-    const uint128 low = tree_indices[i] & w1_mask;
-    for (int64_t sub = 0; sub < (int64_t{1} << s); ++sub) {
-      const int64_t u = (i << s) + sub;
-      if (!from_root) parent[u] = parent_of[i];
-      path[u] = ToBlock(s ? ((low << s) | static_cast<uint128>(sub)) : low);
-      if (sub == 0) save[u] = static_cast<int32_t>(i);
-    }
+  clk.mark(1);
+  // Start-node tables: u = tree index i * 2^s + sub.  Host staging buffers
+  // are reused across calls (no page faults on 1 M-entry levels).
+  static thread_local std::vector<int32_t> tl_parent, tl_save;
+  static thread_local std::vector<dpf_block> tl_path;
+  // Plain references: the worker threads below must write the CALLING
+  // thread's buffers, not their own thread_local instances.
+  std::vector<int32_t>& parent = tl_parent;
+  std::vector<int32_t>& save = tl_save;
+  std::vector<dpf_block>& path = tl_path;
+  if (static_cast<int64_t>(parent.size()) < U) {
+    parent.resize(U);
+    save.resize(U);
+    path.resize(U);
   }
+  const uint128 w1_mask = W1 >= 128 ? ~uint128{0} : ((uint128{1} << W1) - 1);
+  dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      const uint128 low = tree_indices[i] & w1_mask;
+      for (int64_t sub = 0; sub < (int64_t{1} << s); ++sub) {
+        const int64_t u = (i << s) + sub;
+        parent[u] = from_root ? 0 : parent_of[i];
+        path[u] = ToBlock(s ? ((low << s) | static_cast<uint128>(sub)) : low);
+        save[u] = sub == 0 ? static_cast<int32_t>(i) : -1;
+      }
+    }
+  });
+  clk.mark(2);
   DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.parent_, &ctx.parent_cap_, U * sizeof(int32_t)));
   DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.path_, &ctx.path_cap_, U * sizeof(dpf_block)));
   DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.save_, &ctx.save_cap_, U * sizeof(int32_t)));
@@ -245,6 +347,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.offsets_, offsets.data(), P * sizeof(int64_t), stream));
   }
 
+  clk.mark(3);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   auto launch = [&](int sum_mode, void* out, uint64_t* workspace) {
     return FromHip(dpf_hip_eval_prefix_batch(
@@ -296,11 +399,13 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
                                                  ctx.stage_, device_out, stream));
   }
 
+  if (g_timing_on) dpf_hip_stream_sync(stream);  // attribute device time to its phase
+  clk.mark(4);
   // Context update (cc:435-451, 494-496).
   ctx.previous_hierarchy_level_ = hierarchy_level;
   if (P > 0) {
     if (update_ctx) {
-      ctx.partial_prefixes_ = std::move(tree_indices);
+      std::swap(ctx.partial_prefixes_, tree_indices);
       std::swap(ctx.seeds_, ctx.next_seeds_);
       std::swap(ctx.seeds_cap_, ctx.next_seeds_cap_);
       std::swap(ctx.ctrl_, ctx.next_ctrl_);
@@ -310,6 +415,8 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     }
     ctx.partial_evaluations_level_ = prev;
   }
+  ctx.spare_prefixes_ = std::move(tree_indices);
+  clk.mark(5);
   return n;
 }
 

@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "dpf/distributed_point_function.pb.h"
 #include "dpf/internal/value_type_helpers.h"
@@ -65,6 +67,45 @@ struct U128Hash {
     return static_cast<size_t>(x * 0xBF58476D1CE4E5B9ULL);
   }
 };
+
+// fn(lo, hi) over [0, n) split across host threads (at most 16) when n is
+// large enough to pay for them; inline otherwise.
+template <typename F>
+void ParallelFor(int64_t n, F fn, int64_t min_per_thread = int64_t{1} << 15) {
+  int threads = static_cast<int>(std::min<int64_t>(
+      std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency())),
+      n / std::max<int64_t>(min_per_thread, 1)));
+  if (threads <= 1) {
+    if (n > 0) fn(int64_t{0}, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(threads);
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back(fn, n * t / threads, n * (t + 1) / threads);
+  for (auto& th : pool) th.join();
+}
+
+// Number of chunks ParallelChunks uses for n items.
+inline int NumChunks(int64_t n, int64_t min_per_chunk = int64_t{1} << 15) {
+  const int64_t hw = std::max(1u, std::thread::hardware_concurrency());
+  return static_cast<int>(std::max<int64_t>(
+      1, std::min<int64_t>(std::min<int64_t>(16, hw), n / std::max<int64_t>(min_per_chunk, 1))));
+}
+
+// fn(chunk, lo, hi) for `chunks` contiguous chunks of [0, n), one thread each.
+template <typename F>
+void ParallelChunks(int64_t n, int chunks, F fn) {
+  if (chunks <= 1) {
+    fn(0, int64_t{0}, n);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(chunks);
+  for (int c = 0; c < chunks; ++c)
+    pool.emplace_back(fn, c, n * c / chunks, n * (c + 1) / chunks);
+  for (auto& th : pool) th.join();
+}
 
 // A growable device allocation (C-ABI allocator), reused across calls.
 class DeviceBuffer {

@@ -78,10 +78,13 @@ std::vector<int> ComputeLevelsToEvaluate(const std::vector<std::vector<uint128>>
 }
 
 namespace {
-uint64_t Fold(const std::vector<uint32_t>& v) {
+uint64_t Fold(const uint32_t* v, int64_t n) {
   uint64_t h = 0;
-  for (size_t i = 0; i < v.size(); ++i) h ^= (static_cast<uint64_t>(v[i]) << ((i & 1) * 32));
+  for (int64_t i = 0; i < n; ++i) h ^= (static_cast<uint64_t>(v[i]) << ((i & 1) * 32));
   return h;
+}
+uint64_t Fold(const std::vector<uint32_t>& v) {
+  return Fold(v.data(), static_cast<int64_t>(v.size()));
 }
 }  // namespace
 
@@ -132,6 +135,7 @@ StatusOr<HierarchicalResult> RunHierarchicalEvaluationDeviceContext(
     return Status(static_cast<StatusCode>(rc), dpf_hip_last_error());
   HierarchicalResult r;
   Status st = OkStatus();
+  std::unique_ptr<uint32_t[]> host(new uint32_t[std::max<int64_t>(max_bytes / 4, 1)]);
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < num_iterations && st.ok(); ++i) {
     ctx->Reset();
@@ -144,14 +148,14 @@ StatusOr<HierarchicalResult> RunHierarchicalEvaluationDeviceContext(
         st = n.status();
         break;
       }
-      // The reference returns the level's outputs in host memory.
-      std::vector<uint32_t> result(*n);
-      if (int rc = dpf_hip_memcpy_d2h(result.data(), out, *n * 4, nullptr)) {
+      // The reference returns the level's outputs in host memory (one buffer
+      // reused across levels here).
+      if (int rc = dpf_hip_memcpy_d2h(host.get(), out, *n * 4, nullptr)) {
         st = Status(static_cast<StatusCode>(rc), dpf_hip_last_error());
         break;
       }
       r.outputs_per_level.push_back(*n);
-      r.checksum ^= Fold(result);
+      r.checksum ^= Fold(host.get(), *n);
     }
   }
   const auto t1 = std::chrono::steady_clock::now();

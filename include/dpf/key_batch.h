@@ -121,6 +121,7 @@ class DeviceBatchContext {
   int previous_hierarchy_level_ = -1;
   int partial_evaluations_level_ = -1;
   std::vector<uint128> partial_prefixes_;
+  std::vector<uint128> spare_prefixes_;  // recycled storage for the next prefix list
   void* seeds_ = nullptr;  // current partial evaluations
   void* ctrl_ = nullptr;
   size_t seeds_cap_ = 0, ctrl_cap_ = 0;
