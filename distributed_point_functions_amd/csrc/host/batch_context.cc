@@ -162,50 +162,9 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   static thread_local std::vector<std::pair<int64_t, int>> tl_prefix_map;
   std::vector<std::pair<int64_t, int>>& prefix_map = tl_prefix_map;
   prefix_map.clear();
-  if (P > 0) {
-    const int bib = prev_log - hierarchy_to_tree()[prev];
-    tree_indices.reserve(P);
-    prefix_map.reserve(P);
-    const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
-    const int chunks = dpf_internal::NumChunks(P);
-    std::vector<char> chunk_ascending(chunks, 1);
-    dpf_internal::ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
-      for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
-        if (!(prefixes[i - 1] < prefixes[i])) { chunk_ascending[c] = 0; return; }
-    });
-    const bool ascending =
-        std::all_of(chunk_ascending.begin(), chunk_ascending.end(), [](char a) { return a != 0; });
-    if (ascending) {
-      // Equal tree indices are adjacent: a new one starts wherever the tree
-      // index changes.  Two parallel passes: count per chunk, then place.
-      std::vector<int64_t> first(chunks + 1, 0);
-      auto starts = [&](int64_t i) { return i == 0 || (prefixes[i] >> bib) != (prefixes[i - 1] >> bib); };
-      dpf_internal::ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
-        int64_t k = 0;
-        for (int64_t i = lo; i < hi; ++i) k += starts(i);
-        first[c + 1] = k;
-      });
-      for (int c = 0; c < chunks; ++c) first[c + 1] += first[c];
-      tree_indices.resize(first[chunks]);
-      prefix_map.resize(P);
-      dpf_internal::ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
-        int64_t pos = first[c] - 1;
-        for (int64_t i = lo; i < hi; ++i) {
-          if (starts(i)) tree_indices[++pos] = prefixes[i] >> bib;
-          prefix_map[i] = {pos, static_cast<int>(prefixes[i] & bmask)};
-        }
-      });
-    } else {
-      std::unordered_map<uint128, int64_t, U128Hash> inverse;
-      inverse.reserve(P * 2);
-      for (int64_t i = 0; i < P; ++i) {
-        const uint128 ti = prefixes[i] >> bib;
-        auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
-        if (inserted) tree_indices.push_back(ti);
-        prefix_map.emplace_back(it->second, static_cast<int>(prefixes[i] & bmask));
-      }
-    }
-  }
+  if (P > 0)
+    dpf_internal::DedupTreeIndices(prefixes, prev_log - hierarchy_to_tree()[prev], &tree_indices,
+                                   &prefix_map);
 
   clk.mark(0);
   // Where each tree index starts: a stored partial evaluation or the root

@@ -314,30 +314,47 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     const auto& pe = ctx.partial_evaluations();
     const int64_t m = pe.size();
     // Sorted fast path (the usual hierarchical case: both the stored prefixes
-    // and the lookups come out of EvaluateUntil in ascending order): one merge
-    // pass instead of a hash map, with the reference's duplicate check
-    // (cc:365-383) on adjacent equal prefixes and its lookup error (cc:392-407).
-    bool sorted = true;
-    for (int64_t j = 1; j < m && sorted; ++j)
-      sorted = FromProtoBlock(pe[j - 1].prefix()) <= FromProtoBlock(pe[j].prefix());
-    for (int64_t i = 1; i < n && sorted; ++i) sorted = parent_of(i - 1) <= parent_of(i);
+    // and the lookups come out of EvaluateUntil in ascending order): chunked
+    // merge passes on host threads instead of a hash map, with the
+    // reference's duplicate check (cc:365-383) on adjacent equal prefixes and
+    // its lookup error (cc:392-407).
+    std::vector<uint128> stored(m);
+    dpf_internal::ParallelFor(m, [&](int64_t lo, int64_t hi) {
+      for (int64_t j = lo; j < hi; ++j) stored[j] = FromProtoBlock(pe[j].prefix());
+    });
+    const int chunks_m = dpf_internal::NumChunks(m), chunks_n = dpf_internal::NumChunks(n);
+    std::vector<char> ok_m(chunks_m, 1), ok_n(chunks_n, 1);
+    dpf_internal::ParallelChunks(m, chunks_m, [&](int c, int64_t lo, int64_t hi) {
+      for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
+        if (stored[j - 1] > stored[j]) { ok_m[c] = 0; return; }
+    });
+    dpf_internal::ParallelChunks(n, chunks_n, [&](int c, int64_t lo, int64_t hi) {
+      for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
+        if (parent_of(i - 1) > parent_of(i)) { ok_n[c] = 0; return; }
+    });
+    bool sorted = std::all_of(ok_m.begin(), ok_m.end(), [](char x) { return x != 0; }) &&
+                  std::all_of(ok_n.begin(), ok_n.end(), [](char x) { return x != 0; });
     if (sorted) {
       for (int64_t j = 1; j < m; ++j)
-        if (FromProtoBlock(pe[j - 1].prefix()) == FromProtoBlock(pe[j].prefix()) &&
+        if (stored[j - 1] == stored[j] &&
             (FromProtoBlock(pe[j - 1].seed()) != FromProtoBlock(pe[j].seed()) ||
              pe[j - 1].control_bit() != pe[j].control_bit()))
           return InvalidArgumentError(
               "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
-      int64_t j = 0;
-      for (int64_t i = 0; i < n; ++i) {
-        const uint128 want = parent_of(i);
-        while (j < m && FromProtoBlock(pe[j].prefix()) < want) ++j;
-        if (j == m || FromProtoBlock(pe[j].prefix()) != want)
-          return InvalidArgumentError("Prefix not present in ctx.partial_evaluations at hierarchy level " +
-                                      std::to_string(hierarchy_level));
-        seeds[i] = ToBlock(FromProtoBlock(pe[j].seed()));
-        ctrl[i] = pe[j].control_bit();
-      }
+      std::vector<char> missing(chunks_n, 0);
+      dpf_internal::ParallelChunks(n, chunks_n, [&](int c, int64_t lo, int64_t hi) {
+        int64_t j = std::lower_bound(stored.begin(), stored.end(), parent_of(lo)) - stored.begin();
+        for (int64_t i = lo; i < hi; ++i) {
+          const uint128 want = parent_of(i);
+          while (j < m && stored[j] < want) ++j;
+          if (j == m || stored[j] != want) { missing[c] = 1; return; }
+          seeds[i] = ToBlock(FromProtoBlock(pe[j].seed()));
+          ctrl[i] = pe[j].control_bit();
+        }
+      });
+      if (std::any_of(missing.begin(), missing.end(), [](char x) { return x != 0; }))
+        return InvalidArgumentError("Prefix not present in ctx.partial_evaluations at hierarchy level " +
+                                    std::to_string(hierarchy_level));
     } else {
     std::unordered_map<uint128, std::pair<uint128, bool>, U128Hash> previous;
     previous.reserve(ctx.partial_evaluations_size() * 2);
@@ -371,7 +388,9 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   if (before_device) DPF_RETURN_IF_ERROR(before_device());
   auto* s = scratch_.get();
   std::vector<dpf_block> paths(std::max<int64_t>(n, 1));
-  for (int64_t i = 0; i < n; ++i) paths[i] = ToBlock(prefixes[i]);
+  dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) paths[i] = ToBlock(prefixes[i]);
+  });
   DPF_RETURN_IF_ERROR(s->path_seed.Upload(seeds.data(), seeds.size(), stream));
   DPF_RETURN_IF_ERROR(s->path_ctrl.Upload(ctrl.data(), ctrl.size(), stream));
   DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size(), stream));
@@ -386,13 +405,16 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   if (update_ctx) {
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds.data(), s->path_seed.get(), n * sizeof(dpf_block), stream));
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(ctrl.data(), s->path_ctrl.get(), n, stream));
-    ctx.mutable_partial_evaluations()->Reserve(static_cast<int>(n));
-    for (int64_t i = 0; i < n; ++i) {
-      PartialEvaluation* e = ctx.add_partial_evaluations();
-      SetProtoBlock(prefixes[i], e->mutable_prefix());
-      SetProtoBlock(FromBlock(seeds[i]), e->mutable_seed());
-      e->set_control_bit(ctrl[i] != 0);
-    }
+    auto& pes = ctx.mutable_partial_evaluations()->vec();
+    pes.resize(n);
+    dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i) {
+        PartialEvaluation* e = &pes[i];
+        SetProtoBlock(prefixes[i], e->mutable_prefix());
+        SetProtoBlock(FromBlock(seeds[i]), e->mutable_seed());
+        e->set_control_bit(ctrl[i] != 0);
+      }
+    });
   }
   ctx.set_partial_evaluations_level(hierarchy_level);
   out->n = n;
@@ -457,34 +479,11 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   const int64_t num_prefixes = static_cast<int64_t>(prefixes.size());
   std::vector<uint128> tree_indices;
   std::vector<std::pair<int64_t, int>> prefix_map;
-  if (num_prefixes > 0) {
-    const int bib = parameters()[previous_hierarchy_level].log_domain_size() -
-                    hierarchy_to_tree()[previous_hierarchy_level];
-    tree_indices.reserve(num_prefixes);
-    prefix_map.reserve(num_prefixes);
-    bool ascending = true;
-    for (int64_t i = 1; i < num_prefixes && ascending; ++i) ascending = prefixes[i - 1] < prefixes[i];
-    if (ascending) {
-      // Ascending prefixes: equal tree indices are adjacent, first-seen order
-      // is sorted order -- no hash map needed.
-      for (int64_t i = 0; i < num_prefixes; ++i) {
-        uint128 ti = prefixes[i] >> bib;
-        int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
-        if (tree_indices.empty() || tree_indices.back() != ti) tree_indices.push_back(ti);
-        prefix_map.emplace_back(static_cast<int64_t>(tree_indices.size()) - 1, bi);
-      }
-    } else {
-      std::unordered_map<uint128, int64_t, U128Hash> inverse;
-      inverse.reserve(num_prefixes * 2);
-      for (int64_t i = 0; i < num_prefixes; ++i) {
-        uint128 ti = prefixes[i] >> bib;
-        int bi = static_cast<int>(prefixes[i] & ((static_cast<uint128>(1) << bib) - 1));
-        auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices.size()));
-        if (inserted) tree_indices.push_back(ti);
-        prefix_map.emplace_back(it->second, bi);
-      }
-    }
-  }
+  if (num_prefixes > 0)
+    dpf_internal::DedupTreeIndices(prefixes,
+                                   parameters()[previous_hierarchy_level].log_domain_size() -
+                                       hierarchy_to_tree()[previous_hierarchy_level],
+                                   &tree_indices, &prefix_map);
 
   // ExpandAndUpdateContext (cc:455-498): starting seeds on the device.  The
   // value correction of this level (h:761-780) is parsed before device work.

@@ -7,7 +7,11 @@
 #include <algorithm>
 #include <cstring>
 #include <thread>
+#include <unordered_map>
+#include <utility>
 #include <vector>
+
+#include "dpf/span.h"
 
 #include "dpf/distributed_point_function.pb.h"
 #include "dpf/internal/value_type_helpers.h"
@@ -105,6 +109,64 @@ void ParallelChunks(int64_t n, int chunks, F fn) {
   for (int c = 0; c < chunks; ++c)
     pool.emplace_back(fn, c, n * c / chunks, n * (c + 1) / chunks);
   for (auto& th : pool) th.join();
+}
+
+// Unique tree indices (prefix >> bib) of `prefixes` in first-seen order and,
+// per prefix, (position of its tree index, block index) -- EvaluateUntil's
+// dedup (distributed_point_function.h:718-742).  Ascending prefixes (the
+// hierarchical case) take a two-pass parallel scan; anything else a hash map.
+// The output vectors are overwritten (their capacity is reused).
+inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<uint128>* tree_indices,
+                             std::vector<std::pair<int64_t, int>>* prefix_map) {
+  const int64_t P = static_cast<int64_t>(prefixes.size());
+  tree_indices->clear();
+  prefix_map->clear();
+  if (P == 0) return;
+  const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
+  const int chunks = NumChunks(P);
+  std::vector<char> chunk_ascending(chunks, 1);
+  ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
+    for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
+      if (!(prefixes[i - 1] < prefixes[i])) {
+        chunk_ascending[c] = 0;
+        return;
+      }
+  });
+  const bool ascending =
+      std::all_of(chunk_ascending.begin(), chunk_ascending.end(), [](char a) { return a != 0; });
+  if (ascending) {
+    // Equal tree indices are adjacent: count the starts per chunk, scan, place.
+    std::vector<int64_t> first(chunks + 1, 0);
+    auto starts = [&](int64_t i) {
+      return i == 0 || (prefixes[i] >> bib) != (prefixes[i - 1] >> bib);
+    };
+    ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
+      int64_t k = 0;
+      for (int64_t i = lo; i < hi; ++i) k += starts(i);
+      first[c + 1] = k;
+    });
+    for (int c = 0; c < chunks; ++c) first[c + 1] += first[c];
+    tree_indices->resize(first[chunks]);
+    prefix_map->resize(P);
+    ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
+      int64_t pos = first[c] - 1;
+      for (int64_t i = lo; i < hi; ++i) {
+        if (starts(i)) (*tree_indices)[++pos] = prefixes[i] >> bib;
+        (*prefix_map)[i] = {pos, static_cast<int>(prefixes[i] & bmask)};
+      }
+    });
+    return;
+  }
+  std::unordered_map<uint128, int64_t, U128Hash> inverse;
+  inverse.reserve(P * 2);
+  tree_indices->reserve(P);
+  prefix_map->reserve(P);
+  for (int64_t i = 0; i < P; ++i) {
+    const uint128 ti = prefixes[i] >> bib;
+    auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices->size()));
+    if (inserted) tree_indices->push_back(ti);
+    prefix_map->emplace_back(it->second, static_cast<int>(prefixes[i] & bmask));
+  }
 }
 
 // A growable device allocation (C-ABI allocator), reused across calls.

@@ -210,6 +210,15 @@ StatusOr<T> FromValueImpl(const Value& value) {
 // Unpacks n packed elements of T.
 template <typename T>
 std::vector<T> UnpackElements(const FlatValueType& flat, const uint8_t* data, int64_t n) {
+  // Plain unsigned integers: the packed image IS the array of T.
+  if constexpr ((std::is_integral_v<T> && std::is_unsigned_v<T>) || std::is_same_v<T, uint128>) {
+    if (flat.leaves.size() == 1 && flat.packed_size == static_cast<int>(sizeof(T)) &&
+        flat.leaves[0].bits == static_cast<int>(8 * sizeof(T)) && flat.leaves[0].kind == kLeafInt) {
+      std::vector<T> out(n);
+      if (n) std::memcpy(out.data(), data, n * sizeof(T));
+      return out;
+    }
+  }
   std::vector<T> out;
   out.reserve(n);
   std::vector<uint128> leaves(flat.leaves.size());
