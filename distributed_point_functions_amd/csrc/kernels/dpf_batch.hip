@@ -29,6 +29,7 @@
 // registers, then adds them once into exact 192-bit per-element sums.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../../include/dpf_hip.h"
 #include "dpf_device.h"
@@ -233,26 +234,27 @@ struct FastV {
 // int_mod_n.h:155-177): r = first 16 bytes; value_i = r mod N_i; then
 // r = (r / N_i) << 32 | next 4 bytes.  Division by the invariant N_i is the
 // 2-by-1 word algorithm above -- no 128-bit division loop.
+template <int NLMAX, bool ILP4>
 struct Mod32V {
   struct Val {
-    uint32_t x[kMod32MaxLeaves];
+    uint32_t x[NLMAX];
   };
   int nl;
   int b;  // blocks the sampling reads: 1 (one leaf) or 2 (<= 4 leaves of 4 bytes)
-  Div32 div[kMod32MaxLeaves];
+  Div32 div[NLMAX];
   int party;
-  uint32_t c[kMod32MaxLeaves];
+  uint32_t c[NLMAX];
 
   __device__ __forceinline__ void key(const BatchLevelParams& p, int64_t k) {
     party = p.party[k] & 1;
     const dpf_block* v = p.vcw + k * p.vcw_stride;
 #pragma unroll
-    for (int i = 0; i < kMod32MaxLeaves; ++i) c[i] = i < nl ? (uint32_t)v[i].low : 0u;
+    for (int i = 0; i < NLMAX; ++i) c[i] = i < nl ? (uint32_t)v[i].low : 0u;
   }
   __device__ __forceinline__ void convert(const uint32_t* w, uint32_t t, Val& out) const {
     uint32_t blk[4] = {w[0], w[1], w[2], w[3]};
 #pragma unroll
-    for (int i = 0; i < kMod32MaxLeaves; ++i) {
+    for (int i = 0; i < NLMAX; ++i) {
       if (i < nl) {
         uint32_t q[3];
         const uint32_t n = div[i].n;
@@ -273,16 +275,28 @@ struct Mod32V {
                                        uint32_t t0, Block4 s1, uint32_t t1, Val& v0,
                                        Val& v1) const {
     uint32_t w0[8], w1[8];
+    if (ILP4 && b == 2) {
+      // Both leaves' two blocks as one interleaved quadruple.
+      Block4 h[4] = {s0, add_small(s0, 1u), s1, add_small(s1, 1u)};
+      const UniformRK rk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
+                               UniformRK{p.rkv.k}};
+      dpf_aes::mmo_hashN<4>(h, lk, rk);
+      w0[0] = h[0].w0; w0[1] = h[0].w1; w0[2] = h[0].w2; w0[3] = h[0].w3;
+      w0[4] = h[1].w0; w0[5] = h[1].w1; w0[6] = h[1].w2; w0[7] = h[1].w3;
+      w1[0] = h[2].w0; w1[1] = h[2].w1; w1[2] = h[2].w2; w1[3] = h[2].w3;
+      w1[4] = h[3].w0; w1[5] = h[3].w1; w1[6] = h[3].w2; w1[7] = h[3].w3;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j < b) {
-        Block4 h0 = add_small(s0, (uint32_t)j), h1 = add_small(s1, (uint32_t)j);
-        dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
-        w0[4 * j] = h0.w0; w0[4 * j + 1] = h0.w1; w0[4 * j + 2] = h0.w2; w0[4 * j + 3] = h0.w3;
-        w1[4 * j] = h1.w0; w1[4 * j + 1] = h1.w1; w1[4 * j + 2] = h1.w2; w1[4 * j + 3] = h1.w3;
-      } else {
-        w0[4 * j] = w0[4 * j + 1] = w0[4 * j + 2] = w0[4 * j + 3] = 0;
-        w1[4 * j] = w1[4 * j + 1] = w1[4 * j + 2] = w1[4 * j + 3] = 0;
+      for (int j = 0; j < 2; ++j) {
+        if (j < b) {
+          Block4 h0 = add_small(s0, (uint32_t)j), h1 = add_small(s1, (uint32_t)j);
+          dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+          w0[4 * j] = h0.w0; w0[4 * j + 1] = h0.w1; w0[4 * j + 2] = h0.w2; w0[4 * j + 3] = h0.w3;
+          w1[4 * j] = h1.w0; w1[4 * j + 1] = h1.w1; w1[4 * j + 2] = h1.w2; w1[4 * j + 3] = h1.w3;
+        } else {
+          w0[4 * j] = w0[4 * j + 1] = w0[4 * j + 2] = w0[4 * j + 3] = 0;
+          w1[4 * j] = w1[4 * j + 1] = w1[4 * j + 2] = w1[4 * j + 3] = 0;
+        }
       }
     }
     convert(w0, t0, v0);
@@ -305,11 +319,11 @@ struct Mod32V {
   }
   __device__ __forceinline__ static void zero(Val& a) {
 #pragma unroll
-    for (int i = 0; i < kMod32MaxLeaves; ++i) a.x[i] = 0;
+    for (int i = 0; i < NLMAX; ++i) a.x[i] = 0;
   }
   __device__ __forceinline__ void acc_add(Val& a, const Val& v) const {
 #pragma unroll
-    for (int i = 0; i < kMod32MaxLeaves; ++i) {
+    for (int i = 0; i < NLMAX; ++i) {
       if (i < nl) {
         uint32_t s = a.x[i] + v.x[i];
         a.x[i] = (s < a.x[i] || s >= div[i].n) ? s - div[i].n : s;
@@ -318,13 +332,13 @@ struct Mod32V {
   }
   __device__ __forceinline__ void flush(const BatchLevelParams& p, int64_t slot0, const Val& a) const {
 #pragma unroll
-    for (int i = 0; i < kMod32MaxLeaves; ++i)
+    for (int i = 0; i < NLMAX; ++i)
       if (i < nl && a.x[i]) wide_add(p.wide + (slot0 * nl + i) * 3, (u128)a.x[i]);
   }
   __device__ __forceinline__ void store(const LdsLookup&, const BatchLevelParams& p, char* o,
                                         const Val& v) const {
 #pragma unroll
-    for (int i = 0; i < kMod32MaxLeaves; ++i)
+    for (int i = 0; i < NLMAX; ++i)
       if (i < nl) *reinterpret_cast<uint32_t*>(o + 4 * i) = v.x[i];
   }
 };
@@ -585,6 +599,18 @@ int launch_batch(const BatchLevelParams& p, const V& v, hipStream_t s) {
   return kOk;
 }
 
+template <int NLMAX, bool ILP4>
+int launch_mod32(const BatchLevelParams& p, const dpf_value_desc* desc, int b, int sum,
+                 hipStream_t s) {
+  using V = Mod32V<NLMAX, ILP4>;
+  V v;
+  memset(&v, 0, sizeof(v));
+  v.nl = desc->num_leaves;
+  v.b = b;
+  for (int k = 0; k < desc->num_leaves; ++k) v.div[k] = make_div32((uint32_t)desc->mod_low[k]);
+  return sum ? launch_batch<V, 2, true>(p, v, s) : launch_batch<V, 2, false>(p, v, s);
+}
+
 template <bool SUM>
 int launch_batch_fast(const BatchLevelParams& p, int bits, int xor_mode, hipStream_t s) {
   switch (bits) {
@@ -695,12 +721,10 @@ int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_lev
       st = sum ? launch_batch_fast<true>(p, desc->bits[0], xm, s)
                : launch_batch_fast<false>(p, desc->bits[0], xm, s);
     } else if (mod32_eligible(desc, &b)) {
-      Mod32V v;
-      memset(&v, 0, sizeof(v));
-      v.nl = nl;
-      v.b = b;
-      for (int k = 0; k < nl; ++k) v.div[k] = make_div32((uint32_t)desc->mod_low[k]);
-      st = sum ? launch_batch<Mod32V, 2, true>(p, v, s) : launch_batch<Mod32V, 2, false>(p, v, s);
+      // Leaf pairs hash their four blocks as one ILP4 group (r05: +0.8% over
+      // two ILP2 pairs on heavy hitters); tuples of <= 2 leaves use 2-wide
+      // accumulators (117 instead of 128 VGPRs).
+      st = nl <= 2 ? launch_mod32<2, true>(p, desc, b, sum, s) : launch_mod32<4, true>(p, desc, b, sum, s);
     } else {
       GenericV v;
       memset(&v, 0, sizeof(v));
