@@ -229,6 +229,18 @@ class PyDpf {
     return PyKeyBatch{std::make_shared<KeyBatch>(Take(dpf_->MakeKeyBatch(MakeConstSpan(ptrs))))};
   }
   py::bytes KeyFromBatch(const PyKeyBatch& b, int64_t k) { return Ser(Take(dpf_->KeyFromBatch(*b.b, k))); }
+  PyKeyBatch ParseKeyBatch(const std::vector<py::bytes>& keys, int threads) {
+    std::vector<std::string_view> views;
+    views.reserve(keys.size());
+    for (const auto& b : keys)
+      views.emplace_back(PyBytes_AS_STRING(b.ptr()), static_cast<size_t>(PyBytes_GET_SIZE(b.ptr())));
+    StatusOr<KeyBatch> r = InternalError("unset");
+    {
+      py::gil_scoped_release nogil;
+      r = dpf_->ParseKeyBatch(Span<const std::string_view>(views), threads);
+    }
+    return PyKeyBatch{std::make_shared<KeyBatch>(Take(std::move(r)))};
+  }
   py::tuple GenerateKeyBatch(const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& alphas,
                              const std::vector<py::bytes>& betas, const py::object& root_seeds,
                              int threads) {
@@ -416,6 +428,7 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("evaluate_at_batch", &PyDpf::EvaluateAtBatch)
       .def("make_key_batch", &PyDpf::MakeKeyBatch)
       .def("key_from_batch", &PyDpf::KeyFromBatch)
+      .def("parse_key_batch", &PyDpf::ParseKeyBatch)
       .def("generate_key_batch", &PyDpf::GenerateKeyBatch)
       .def("evaluate_at_batch_to_device", &PyDpf::EvaluateAtBatchToDevice)
       .def("evaluate_at_batch_sum_to_device", &PyDpf::EvaluateAtBatchSumToDevice)

@@ -73,39 +73,95 @@ DeviceKeyBatch::~DeviceKeyBatch() {
 }
 
 // ------------------------------------------------------------ ingestion
-StatusOr<KeyBatch> DistributedPointFunction::MakeKeyBatch(Span<const DpfKey* const> keys) const {
+void DistributedPointFunction::ResizeKeyBatch(int64_t n, KeyBatch* b) const {
   const int H = static_cast<int>(parameters().size());
   const int L = tree_levels_needed() - 1;
-  KeyBatch b;
-  b.num_keys = static_cast<int64_t>(keys.size());
-  b.num_levels = L;
-  b.seed.resize(b.num_keys);
-  b.party.resize(b.num_keys);
-  b.cw_seed.resize(b.num_keys * L);
-  b.cw_left.resize(b.num_keys * L);
-  b.cw_right.resize(b.num_keys * L);
-  b.value_correction.resize(H);
+  b->num_keys = n;
+  b->num_levels = L;
+  b->seed.resize(n);
+  b->party.resize(n);
+  b->cw_seed.resize(n * L);
+  b->cw_left.resize(n * L);
+  b->cw_right.resize(n * L);
+  b->value_correction.resize(H);
   for (int h = 0; h < H; ++h) {
     const auto& f = flat_value_type(h);
-    b.value_correction[h].resize(b.num_keys * f.elements_per_block * f.leaves.size());
+    b->value_correction[h].resize(n * f.elements_per_block * f.leaves.size());
   }
-  for (int64_t k = 0; k < b.num_keys; ++k) {
-    const DpfKey& key = *keys[k];
-    DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
-    b.seed[k] = ToBlock(FromProtoBlock(key.seed()));
-    b.party[k] = static_cast<uint8_t>(key.party() & 1);
-    for (int j = 0; j < L; ++j) {
-      const CorrectionWord& cw = key.correction_words(j);
-      b.cw_seed[k * L + j] = ToBlock(FromProtoBlock(cw.seed()));
-      b.cw_left[k * L + j] = cw.control_left();
-      b.cw_right[k * L + j] = cw.control_right();
-    }
-    for (int h = 0; h < H; ++h) {
-      DPF_ASSIGN_OR_RETURN(std::vector<uint128> v, ValueCorrectionLeaves(key, h));
-      auto& dst = b.value_correction[h];
-      for (size_t i = 0; i < v.size(); ++i) dst[k * v.size() + i] = ToBlock(v[i]);
-    }
+}
+
+Status DistributedPointFunction::FillKeyBatchRow(const DpfKey& key, int64_t k, KeyBatch* b) const {
+  const int H = static_cast<int>(parameters().size());
+  const int L = b->num_levels;
+  DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
+  b->seed[k] = ToBlock(FromProtoBlock(key.seed()));
+  b->party[k] = static_cast<uint8_t>(key.party() & 1);
+  for (int j = 0; j < L; ++j) {
+    const CorrectionWord& cw = key.correction_words(j);
+    b->cw_seed[k * L + j] = ToBlock(FromProtoBlock(cw.seed()));
+    b->cw_left[k * L + j] = cw.control_left();
+    b->cw_right[k * L + j] = cw.control_right();
   }
+  for (int h = 0; h < H; ++h) {
+    DPF_ASSIGN_OR_RETURN(std::vector<uint128> v, ValueCorrectionLeaves(key, h));
+    auto& dst = b->value_correction[h];
+    for (size_t i = 0; i < v.size(); ++i) dst[k * v.size() + i] = ToBlock(v[i]);
+  }
+  return OkStatus();
+}
+
+namespace {
+// Runs fill(k) for k < n on up to `threads` host threads; returns the status
+// of the first (lowest k) failure.
+template <typename F>
+Status ParallelRows(int64_t n, int threads, F fill) {
+  int t = threads > 0 ? threads : static_cast<int>(std::thread::hardware_concurrency());
+  t = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({t, 16, (n + 1023) / 1024})));
+  std::vector<Status> first(t, OkStatus());
+  std::vector<int64_t> where(t, n);
+  auto work = [&](int w) {
+    for (int64_t k = n * w / t, hi = n * (w + 1) / t; k < hi; ++k) {
+      Status st = fill(k);
+      if (!st.ok()) {
+        first[w] = st;
+        where[w] = k;
+        return;
+      }
+    }
+  };
+  if (t == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> pool;
+    for (int w = 0; w < t; ++w) pool.emplace_back(work, w);
+    for (auto& th : pool) th.join();
+  }
+  int best = -1;
+  for (int w = 0; w < t; ++w)
+    if (!first[w].ok() && (best < 0 || where[w] < where[best])) best = w;
+  return best < 0 ? OkStatus() : first[best];
+}
+}  // namespace
+
+StatusOr<KeyBatch> DistributedPointFunction::MakeKeyBatch(Span<const DpfKey* const> keys) const {
+  KeyBatch b;
+  const int64_t n = static_cast<int64_t>(keys.size());
+  ResizeKeyBatch(n, &b);
+  DPF_RETURN_IF_ERROR(ParallelRows(n, 0, [&](int64_t k) { return FillKeyBatchRow(*keys[k], k, &b); }));
+  return b;
+}
+
+StatusOr<KeyBatch> DistributedPointFunction::ParseKeyBatch(Span<const std::string_view> serialized,
+                                                           int num_threads) const {
+  KeyBatch b;
+  const int64_t n = static_cast<int64_t>(serialized.size());
+  ResizeKeyBatch(n, &b);
+  DPF_RETURN_IF_ERROR(ParallelRows(n, num_threads, [&](int64_t k) -> Status {
+    DpfKey key;
+    if (!key.ParseFromArray(serialized[k].data(), static_cast<int>(serialized[k].size())))
+      return InvalidArgumentError("Failed to parse DpfKey " + std::to_string(k));
+    return FillKeyBatchRow(key, k, &b);
+  }));
   return b;
 }
 

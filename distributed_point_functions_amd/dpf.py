@@ -340,6 +340,11 @@ class DistributedPointFunction:
         """SoA image of `keys` (host); .upload(begin, end, stream) puts rows on the GPU."""
         return _call(self._impl.make_key_batch, [k.SerializeToString() for k in keys])
 
+    def parse_key_batch(self, serialized_keys: Sequence[bytes], threads: int = 0):
+        """SoA key batch straight from serialized DpfKeys, parsed and validated
+        on host threads (batched key ingestion)."""
+        return _call(self._impl.parse_key_batch, list(serialized_keys), int(threads))
+
     def key_from_batch(self, batch, k: int) -> pb.DpfKey:
         key = pb.DpfKey()
         key.ParseFromString(_call(self._impl.key_from_batch, batch, int(k)))

@@ -29,6 +29,7 @@
 #include <memory>
 #include <set>
 #include <string>
+#include <string_view>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -217,6 +218,12 @@ class DistributedPointFunction {
   // ---- key batches ------------------
   // SoA image of `keys` (each validated like CreateEvaluationContext does).
   StatusOr<KeyBatch> MakeKeyBatch(Span<const DpfKey* const> keys) const;
+  // SoA image of serialized DpfKeys (the proto wire format), parsed and
+  // validated on `num_threads` host threads (0 = hardware concurrency, at most
+  // 16) -- the batched key ingestion of SURVEY.md 8f.2.  Errors name the first
+  // failing key.
+  StatusOr<KeyBatch> ParseKeyBatch(Span<const std::string_view> serialized_keys,
+                                   int num_threads = 0) const;
   // Row k of `batch` as a DpfKey proto (inverse of MakeKeyBatch).
   StatusOr<DpfKey> KeyFromBatch(const KeyBatch& batch, int64_t k) const;
   // Key generation for many alphas at once, straight into SoA form, on
@@ -327,6 +334,9 @@ class DistributedPointFunction {
                                    DeviceStart* out, void* stream,
                                    const std::function<Status()>& before_device) const;
   StatusOr<std::vector<uint128>> ValueCorrectionLeaves(const DpfKey& key, int h) const;
+  // Sizes `b` for n keys, and fills row k from `key` (validated).
+  void ResizeKeyBatch(int64_t n, KeyBatch* b) const;
+  Status FillKeyBatchRow(const DpfKey& key, int64_t k, KeyBatch* b) const;
   // Shared core of the two batched EvaluateUntil entry points.
   StatusOr<int64_t> EvaluateUntilBatchCore(int hierarchy_level, Span<const uint128> prefixes,
                                            DeviceBatchContext& ctx, bool sum, void* device_out,

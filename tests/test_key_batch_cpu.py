@@ -154,3 +154,24 @@ def test_sum_packed_shares_matches_oracle_group_sum(vt):
     for r in range(1, num_shares):
         want = O.add_packed(vt, want, shares[r])
     np.testing.assert_array_equal(got, want)
+
+
+def test_parse_key_batch_matches_make_key_batch():
+    # Batched ingestion of serialized keys == MakeKeyBatch of
+    # the parsed protos, on several threads; the first bad key is reported.
+    levels = [(10, ("int", 16), 0), (40, ("tuple", [("int", 32), ("intmodn", 64, G.M64)]), 48.0)]
+    dpf = make(levels)
+    rng = np.random.default_rng(4)
+    alphas = [int(a) for a in rng.integers(0, 1 << 40, size=3000)]
+    b0, _ = dpf.generate_key_batch(alphas, betas_for(levels), root_seeds=seeds_array(rng, 3000),
+                                   threads=4)
+    keys = [dpf.key_from_batch(b0, k) for k in range(3000)]
+    parsed = dpf.parse_key_batch([k.SerializeToString() for k in keys], threads=4)
+    made = dpf.make_key_batch(keys)
+    assert np.array_equal(parsed.seeds(), made.seeds())
+    for k in (0, 1234, 2999):
+        assert dpf.key_from_batch(parsed, k) == keys[k]
+    bad = [k.SerializeToString() for k in keys[:2500]]
+    bad[1700] = b"\xff\xff\xff"
+    with pytest.raises(D.DpfStatusError, match="Failed to parse DpfKey 1700"):
+        dpf.parse_key_batch(bad, threads=4)
