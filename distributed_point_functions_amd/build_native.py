@@ -33,9 +33,10 @@ HIP_FLAGS = [
     # reads in flight per wave instead of 2-3 (tools/variant_bench.py, r04:
     # batched points 76 -> 89 G AES/s, expand 82 -> 84).
     "-mllvm", "-amdgpu-sched-strategy=iterative-ilp",
-    # Full-domain expansion finishes each subtree in leaf quads (the last 8 AES
-    # of every 10 as ILP4): expand 87.5 -> 89.2 G AES/s (tools/variant_bench.py, r05).
-    "-DDPF_LEAF_QUADS",
+    # -DDPF_LEAF_QUADS (leaf quads, the last 8 AES of every 10 as ILP4) is
+    # available but off: +1.9% same-box in tools/variant_bench.py, but it
+    # spills 88 B/lane and the scratch traffic doubles the kernel's HBM bytes
+    # (profiled r06: 16.5 GB/launch vs 8.9-10.7 GB).
 ]
 
 # Translation units built with LLVM's default scheduler: with iterative-ilp,
