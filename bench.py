@@ -190,6 +190,29 @@ def profiled_traffic(leaves_per_launch: int):
     return best
 
 
+def init_ranks(torch, dist):
+    """One process per GPU (RANK/LOCAL_RANK/WORLD_SIZE from torch.distributed.run),
+    RCCL process group for N > 1.  Returns (world, rank, local, coll), `coll`
+    the device for collective scalars (None: host tensors).
+    DPF_BENCH_ONE_GPU=1 rehearses the N-rank path on a one-GPU box: every rank
+    on cuda:0, a gloo group (RCCL refuses two ranks on one device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    one_gpu = os.environ.get("DPF_BENCH_ONE_GPU") == "1"
+    if one_gpu:
+        local = 0
+    coll = None
+    if world > 1:
+        torch.cuda.set_device(local)
+        if one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            coll = torch.device("cuda", local)
+    return world, rank, local, coll
+
+
 def main():
     args = parse()
     if args.workload.startswith("evaluate_at"):
@@ -209,14 +232,9 @@ def main():
     from distributed_point_functions_amd import proto as pb
     from distributed_point_functions_amd import sharding as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.gpus != int(os.environ.get("WORLD_SIZE", "1")) and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    world, rank, local, coll = init_ranks(torch, dist)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -264,8 +282,8 @@ def main():
     if world > 1:
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
-    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
-    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+    elapsed = S.max_over_ranks(t1 - t0, device=coll)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
 
     # Spot-check the last step's output (sum of the two parties' shares is beta
     # at alpha, 0 elsewhere) on a few positions of this rank's shard.
@@ -367,12 +385,7 @@ def main_evaluate_at(args):
     from distributed_point_functions_amd import proto as pb
     from distributed_point_functions_amd import sharding as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local, coll = init_ranks(torch, dist)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -439,8 +452,8 @@ def main_evaluate_at(args):
     if world > 1:
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
-    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
-    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+    elapsed = S.max_over_ranks(t1 - t0, device=coll)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
 
     # Correctness spot checks outside the timed region.
     if summed:
@@ -579,12 +592,7 @@ def main_heavy_hitters(args):
     from distributed_point_functions_amd import hip_abi as H
     from distributed_point_functions_amd import sharding as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local, coll = init_ranks(torch, dist)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -643,8 +651,8 @@ def main_heavy_hitters(args):
     if world > 1:
         dist.barrier()
     kern_ms = sum(a.elapsed_ms(b) for a, b in evs) / args.steps
-    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
-    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+    elapsed = S.max_over_ranks(t1 - t0, device=coll)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
     if rank == 0:
         HH.verify(record, logs, values, idx)        # every level, untimed
     outputs_per_pass = sum(len(v) for _, v, _, _ in record) * n_keys * 2
@@ -703,12 +711,7 @@ def main_dcf(args):
     from distributed_point_functions_amd import proto as pb
     from distributed_point_functions_amd import sharding as S
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local, coll = init_ranks(torch, dist)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -760,8 +763,8 @@ def main_dcf(args):
     if world > 1:
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
-    elapsed = S.max_over_ranks(t1 - t0, device=dev if world > 1 else None)
-    kern_ms_max = S.max_over_ranks(kern_ms, device=dev if world > 1 else None)
+    elapsed = S.max_over_ranks(t1 - t0, device=coll)
+    kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
     # Spot check against the single-key API (itself parity-tested vs the oracle).
     host_pts = pts.cpu().numpy().view(np.uint64)
     for k in (0, nk - 1):

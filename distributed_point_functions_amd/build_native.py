@@ -132,9 +132,23 @@ def build_oracle(force=False):
     return out
 
 
+def build_tools(force=False):
+    """C++ programs written against the drop-in API (tools/*.cc): the
+    reference's benchmark suite restated (dpf_benchmark)."""
+    src = os.path.join(ROOT, "tools", "dpf_benchmark.cc")
+    out = os.path.join(LIBDIR, "dpf_benchmark")
+    hdrs = _files(os.path.join(INCLUDE), (".h",))
+    if force or _stale(out, [src, os.path.join(LIBDIR, "libdpf.so")] + hdrs):
+        cxx = os.environ.get("CXX", "g++")
+        _run([cxx, "-O2", "-std=c++20", "-Wall", f"-I{INCLUDE}", src, "-o", out, f"-L{LIBDIR}",
+              "-ldpf", "-ldpf_hip", "-Wl,-rpath,$ORIGIN"])
+    return out
+
+
 def build_all(force=False):
     build_hip(force)
     build_host(force)
+    build_tools(force)
     build_oracle(force)
 
 

@@ -293,9 +293,9 @@ Status UploadCorrectionWords(const DpfKey& key, int start, int stop,
     cl[j] = cw.control_left();
     cr[j] = cw.control_right();
   }
-  DPF_RETURN_IF_ERROR(s->cw_seed.Upload(seeds.data(), seeds.size(), stream));
-  DPF_RETURN_IF_ERROR(s->cw_left.Upload(cl.data(), cl.size(), stream));
-  return s->cw_right.Upload(cr.data(), cr.size(), stream);
+  DPF_RETURN_IF_ERROR(s->Upload(s->cw_seed, seeds.data(), seeds.size(), stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->cw_left, cl.data(), cl.size(), stream));
+  return s->Upload(s->cw_right, cr.data(), cr.size(), stream);
 }
 }  // namespace
 
@@ -391,9 +391,9 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) paths[i] = ToBlock(prefixes[i]);
   });
-  DPF_RETURN_IF_ERROR(s->path_seed.Upload(seeds.data(), seeds.size(), stream));
-  DPF_RETURN_IF_ERROR(s->path_ctrl.Upload(ctrl.data(), ctrl.size(), stream));
-  DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size(), stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->path_seed, seeds.data(), seeds.size(), stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->path_ctrl, ctrl.data(), ctrl.size(), stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->paths, paths.data(), paths.size(), stream));
   DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), start_level, stop_level, s, stream));
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight);
   HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(
@@ -439,7 +439,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
                                                    EvaluationContext& ctx,
                                                    const ValueType* requested_type,
                                                    void* device_out, int64_t capacity_bytes,
-                                                   void* stream, std::vector<uint8_t>* host_out,
+                                                   void* stream, const HostSink* host_out,
                                                    int64_t* num_elements) const {
   // h:641-837
   DPF_RETURN_IF_ERROR(validator_->ValidateEvaluationContext(ctx));
@@ -499,8 +499,8 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     DPF_RETURN_IF_ERROR(parse_vcw());
     dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
     uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
-    DPF_RETURN_IF_ERROR(s->start_seed.Upload(&root, 1, stream));
-    DPF_RETURN_IF_ERROR(s->start_ctrl.Upload(&party, 1, stream));
+    DPF_RETURN_IF_ERROR(s->Upload(s->start_seed, &root, 1, stream));
+    DPF_RETURN_IF_ERROR(s->Upload(s->start_ctrl, &party, 1, stream));
     start.n = 1;
     start.seeds = s->start_seed.as<dpf_block>();
     start.ctrl = s->start_ctrl.as<uint8_t>();
@@ -525,7 +525,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
 
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw_blocks.data(), vcw_blocks.size(), stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw_blocks.data(), vcw_blocks.size(), stream));
   DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), start_level, stop_level, s, stream));
 
   // Is the gather (h:822-835) the identity?  Yes when every prefix maps to its
@@ -558,7 +558,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     for (int64_t i = 0; i < num_prefixes; ++i)
       offsets[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
                    prefix_map[i].second * outputs_per_prefix;
-    DPF_RETURN_IF_ERROR(s->offsets.Upload(offsets.data(), offsets.size(), stream));
+    DPF_RETURN_IF_ERROR(s->Upload(s->offsets, offsets.data(), offsets.size(), stream));
     if (device_out) {
       if (capacity_bytes < total * esz) return InvalidArgumentError("device output buffer too small");
       result = device_out;
@@ -570,8 +570,9 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
                                        s->offsets.as<int64_t>(), expand_out, result, stream));
   }
   if (!device_out) {
-    host_out->resize(static_cast<size_t>(total) * esz);
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(host_out->data(), result, host_out->size(), stream));
+    const size_t bytes = static_cast<size_t>(total) * esz;
+    void* dst = (*host_out)(bytes);
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(dst, result, bytes, stream));
   }
   return OkStatus();
 }
@@ -581,9 +582,23 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateUntilPacked(
     const ValueType* requested_type) const {
   std::vector<uint8_t> out;
   int64_t n = 0;
+  const HostSink sink = [&out](size_t bytes) -> void* {
+    out = dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(bytes));
+    return out.data();
+  };
   DPF_RETURN_IF_ERROR(EvaluateUntilCore(hierarchy_level, prefixes, ctx, requested_type, nullptr, 0,
-                                        nullptr, &out, &n));
+                                        nullptr, &sink, &n));
   return out;
+}
+
+Status DistributedPointFunction::EvaluateUntilToHost(int hierarchy_level,
+                                                     Span<const uint128> prefixes,
+                                                     EvaluationContext& ctx,
+                                                     const ValueType* requested_type,
+                                                     const HostSink& sink) const {
+  int64_t n = 0;
+  return EvaluateUntilCore(hierarchy_level, prefixes, ctx, requested_type, nullptr, 0, nullptr,
+                           &sink, &n);
 }
 
 StatusOr<int64_t> DistributedPointFunction::EvaluateUntilToDevice(
@@ -627,9 +642,9 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
   dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
   uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
   dpf_block path = ToBlock(static_cast<uint128>(shard));
-  DPF_RETURN_IF_ERROR(s->start_seed.Upload(&root, 1, stream));
-  DPF_RETURN_IF_ERROR(s->start_ctrl.Upload(&party, 1, stream));
-  DPF_RETURN_IF_ERROR(s->paths.Upload(&path, 1, stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->start_seed, &root, 1, stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->start_ctrl, &party, 1, stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->paths, &path, 1, stream));
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   if (k > 0) {
     DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), 0, k, s, stream));
@@ -642,7 +657,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
   }
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw_blocks.data(), vcw_blocks.size(), stream));
+  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw_blocks.data(), vcw_blocks.size(), stream));
   DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), k, stop_level, s, stream));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   HIP_RETURN_IF_ERROR(dpf_hip_expand(1, s->start_seed.as<dpf_block>(), s->start_ctrl.as<uint8_t>(),
@@ -705,16 +720,16 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
   }
   std::vector<dpf_block> paths(n);
   for (int64_t i = 0; i < n; ++i) paths[i] = ToBlock(tree_indices[i]);
-  DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size()));
-  DPF_RETURN_IF_ERROR(s->block_index.Upload(block_index.data(), block_index.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->paths, paths.data(), paths.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->block_index, block_index.data(), block_index.size()));
   DPF_RETURN_IF_ERROR(UploadCorrectionWords(key, start_level, stop_level, s, nullptr));
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw_blocks.data(), vcw_blocks.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw_blocks.data(), vcw_blocks.size()));
   dpf_block root = ToBlock(FromProtoBlock(key.seed()));
   uint8_t party = static_cast<uint8_t>(key.party() & 1);
-  DPF_RETURN_IF_ERROR(s->key_seed.Upload(&root, 1));
-  DPF_RETURN_IF_ERROR(s->party.Upload(&party, 1));
+  DPF_RETURN_IF_ERROR(s->Upload(s->key_seed, &root, 1));
+  DPF_RETURN_IF_ERROR(s->Upload(s->party, &party, 1));
   DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
@@ -724,7 +739,8 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
       s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
       s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc, s->vcw.as<dpf_block>(), s->out.get(),
       nullptr));
-  std::vector<uint8_t> out(static_cast<size_t>(n) * f.packed_size);
+  std::vector<uint8_t> out =
+      dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(n) * f.packed_size);
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return out;
@@ -777,14 +793,14 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtBatchPacked(
     if (E > 1) block_index[i] = static_cast<int32_t>(points[i] & ((static_cast<uint128>(1) << bib) - 1));
   }
   auto* s = scratch_.get();
-  DPF_RETURN_IF_ERROR(s->key_seed.Upload(seeds.data(), seeds.size()));
-  DPF_RETURN_IF_ERROR(s->party.Upload(party.data(), party.size()));
-  DPF_RETURN_IF_ERROR(s->cw_seed.Upload(cw_seed.data(), cw_seed.size()));
-  DPF_RETURN_IF_ERROR(s->cw_left.Upload(cl.data(), cl.size()));
-  DPF_RETURN_IF_ERROR(s->cw_right.Upload(cr.data(), cr.size()));
-  DPF_RETURN_IF_ERROR(s->vcw.Upload(vcw.data(), vcw.size()));
-  DPF_RETURN_IF_ERROR(s->paths.Upload(paths.data(), paths.size()));
-  DPF_RETURN_IF_ERROR(s->block_index.Upload(block_index.data(), block_index.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->key_seed, seeds.data(), seeds.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->party, party.data(), party.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->cw_seed, cw_seed.data(), cw_seed.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->cw_left, cl.data(), cl.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->cw_right, cr.data(), cr.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw.data(), vcw.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->paths, paths.data(), paths.size()));
+  DPF_RETURN_IF_ERROR(s->Upload(s->block_index, block_index.data(), block_index.size()));
   DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
@@ -793,7 +809,8 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtBatchPacked(
       s->paths.as<dpf_block>(), s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(),
       s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc,
       s->vcw.as<dpf_block>(), s->out.get(), nullptr));
-  std::vector<uint8_t> out(static_cast<size_t>(n) * f.packed_size);
+  std::vector<uint8_t> out =
+      dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(n) * f.packed_size);
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
   return out;
 }

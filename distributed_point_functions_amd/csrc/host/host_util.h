@@ -204,11 +204,70 @@ class DeviceBuffer {
   size_t cap_ = 0;
 };
 
+// Small uploads go through one page-locked ring: the bytes are copied into
+// it and the H2D copy is queued without waiting, so the kernel that consumes
+// them follows on the same stream (a call used to pay one copy + stream
+// synchronisation per argument array, ~18 us each).  The ring wraps only
+// after every stream that copied from it has been synchronised.  Uploads
+// larger than kMaxStaged take the synchronous pageable path.
+class HostStaging {
+ public:
+  static constexpr size_t kMaxStaged = size_t{4} << 20;
+  HostStaging() = default;
+  HostStaging(const HostStaging&) = delete;
+  HostStaging& operator=(const HostStaging&) = delete;
+  ~HostStaging() {
+    if (p_) {
+      (void)Drain();
+      dpf_hip_host_free(p_);
+    }
+  }
+  Status Upload(DeviceBuffer& dst, const void* data, size_t bytes, void* stream) {
+    DPF_RETURN_IF_ERROR(dst.Reserve(bytes));
+    if (bytes == 0) return OkStatus();
+    if (bytes > kMaxStaged) return FromHip(dpf_hip_memcpy_h2d(dst.get(), data, bytes, stream));
+    if (used_ + bytes > cap_) {
+      DPF_RETURN_IF_ERROR(Drain());
+      used_ = 0;
+      if (bytes > cap_) {
+        if (p_) dpf_hip_host_free(p_);
+        p_ = nullptr;
+        cap_ = 0;
+        const size_t want = std::max<size_t>(kMaxStaged, bytes);
+        HIP_RETURN_IF_ERROR(dpf_hip_host_alloc(&p_, want));
+        cap_ = want;
+      }
+    }
+    char* src = static_cast<char*>(p_) + used_;
+    std::memcpy(src, data, bytes);
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(dst.get(), src, bytes, stream));
+    used_ += (bytes + 255) & ~size_t{255};
+    if (std::find(streams_.begin(), streams_.end(), stream) == streams_.end())
+      streams_.push_back(stream);
+    return OkStatus();
+  }
+
+ private:
+  Status Drain() {
+    for (void* st : streams_) HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(st));
+    streams_.clear();
+    return OkStatus();
+  }
+  void* p_ = nullptr;
+  size_t cap_ = 0, used_ = 0;
+  std::vector<void*> streams_;   // streams with copies from the ring since it last wrapped
+};
+
 class DeviceScratch {
  public:
   DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
   DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;
   DeviceBuffer key_seed, party, block_index, workspace;
+  HostStaging staging;
+  template <typename T>
+  Status Upload(DeviceBuffer& dst, const T* data, size_t count, void* stream = nullptr) {
+    return staging.Upload(dst, data, count * sizeof(T), stream);
+  }
 };
 
 }  // namespace dpf_internal

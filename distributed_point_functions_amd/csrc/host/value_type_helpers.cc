@@ -3,8 +3,12 @@
 // dpf/internal/value_type_helpers.{h,cc} and dpf/int_mod_n.{h,cc} unless noted).
 #include "dpf/internal/value_type_helpers.h"
 
+#include <sys/mman.h>
+
 #include <cmath>
 #include <string>
+
+#include "host_util.h"
 
 namespace distributed_point_functions {
 namespace dpf_internal {
@@ -370,6 +374,18 @@ void UnpackLeaves(const FlatValueType& flat, const uint8_t* in, uint128* leaves)
     leaves[k] = LoadLE(in, lb);
     in += lb;
   }
+}
+
+void AdviseHugePages(void* p, size_t bytes) {
+  constexpr uintptr_t kHuge = uintptr_t{2} << 20;
+  if (!p || bytes < (size_t{4} << 20)) return;
+  const uintptr_t lo = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+  if (hi > lo) (void)madvise(reinterpret_cast<void*>(lo), hi - lo, MADV_HUGEPAGE);
+}
+
+void ParallelRanges(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
+  ParallelChunks(n, NumChunks(n, grain), [&fn](int, int64_t lo, int64_t hi) { fn(lo, hi); });
 }
 
 }  // namespace dpf_internal

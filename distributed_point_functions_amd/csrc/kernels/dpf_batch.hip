@@ -593,8 +593,9 @@ bool mod32_eligible(const dpf_value_desc* d, int* blocks_read) {
 
 template <class V, int MAXE, bool SUM>
 int launch_batch(const BatchLevelParams& p, const V& v, hipStream_t s) {
-  hipLaunchKernelGGL((batch_level_kernel<V, MAXE, SUM>), dim3(grid_for(p.num_threads)),
-                     dim3(kBlock), 0, s, p, v);
+  const int blk = block_for(p.num_threads);
+  hipLaunchKernelGGL((batch_level_kernel<V, MAXE, SUM>), dim3(grid_for(p.num_threads, blk)),
+                     dim3(blk), 0, s, p, v);
   HIP_TRY(hipGetLastError());
   return kOk;
 }
@@ -980,7 +981,8 @@ extern "C" int dpf_hip_dcf_eval_batch(int64_t num_keys, int64_t points_per_key, 
   g.elements_per_leaf = 1;
   g.esz = p.esz;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid(grid_for(items)), block(kBlock);
+  const int blk = block_for(items);
+  const dim3 grid(grid_for(items, blk)), block(blk);
   if (fast) {
     switch (desc->bits[0]) {
       case 8: hipLaunchKernelGGL((dcf_eval_kernel<8, true>), grid, block, 0, s, p, lv, g); break;

@@ -24,6 +24,9 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <mutex>
+#include <thread>
+#include <vector>
 #include <string>
 
 #include "../../../include/dpf_hip.h"
@@ -415,8 +418,20 @@ int num_cus() {
   return cus;
 }
 
-int grid_for(int64_t work_items) {
-  int64_t g = (work_items + kBlock - 1) / kBlock;
+int block_for(int64_t work_items) {
+  // A launch smaller than one full workgroup per CU runs LDS-bound on the few
+  // CUs it occupies: give each CU a smaller workgroup instead (the tables cost
+  // ~1 us to fill whatever the workgroup size).
+  const int64_t cus = num_cus();
+  int64_t per_cu = (work_items + cus - 1) / cus;
+  int64_t b = (per_cu + 63) / 64 * 64;
+  if (b < 64) b = 64;
+  if (b > kBlock) b = kBlock;
+  return (int)b;
+}
+
+int grid_for(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
   int64_t cap = num_cus();  // one 128 KiB-LDS workgroup per CU
   if (g > cap) g = cap;
   if (g < 1) g = 1;
@@ -458,7 +473,8 @@ namespace {
 
 template <class Leaf>
 int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
-  hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid_for(p.num_items)), dim3(kBlock), 0, s, p,
+  const int blk = block_for(p.num_items);
+  hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid_for(p.num_items, blk)), dim3(blk), 0, s, p,
                      leaf);
   HIP_TRY(hipGetLastError());
   return kOk;
@@ -474,7 +490,8 @@ int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf
 
 template <class Leaf, int BITS, bool FAST, bool SUM>
 int launch_points_t(const PointParams& p, const Leaf& leaf, hipStream_t s) {
-  const dim3 grid(grid_for(p.num_items)), block(kBlock);
+  const int blk = block_for(p.num_items);
+  const dim3 grid(grid_for(p.num_items, blk)), block(blk);
   if (p.half % 64 == 0)
     hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, true, SUM>), grid, block, 0, s, p, leaf);
   else
@@ -564,6 +581,92 @@ int dpf_hip_set_device(int device) {
   HIP_TRY(hipSetDevice(device));
   return kOk;
 }
+}  // extern "C"
+
+namespace {
+// Large copies between the device and pageable host memory: the runtime pins
+// the user pages for each such copy, which measured ~28 ms per call for
+// 4-128 MiB (tools/dpf_benchmark, BM_EvaluateRegularDpf at 2^22+ outputs)
+// against ~0.3 ms for 16 MiB through page-locked memory.  They go through two
+// page-locked 16 MiB bounce buffers instead, the DMA of one chunk overlapping
+// the host copy of the other.
+constexpr size_t kBounceMin = size_t{2} << 20;
+constexpr size_t kBounceChunk = size_t{16} << 20;
+
+// memcpy on up to 8 host threads for pieces of >= 2 MiB (the host side of a
+// bounce runs at ~28 GB/s on 8 threads vs ~5 on one, page faults included).
+void host_copy(void* dst, const void* src, size_t bytes) {
+  const size_t piece = size_t{2} << 20;
+  size_t t = bytes / piece;
+  const size_t hw = std::thread::hardware_concurrency();
+  if (t > 8) t = 8;
+  if (hw && t > hw) t = hw;
+  if (t <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (size_t i = 0; i < t; ++i) {
+    const size_t lo = bytes * i / t, hi = bytes * (i + 1) / t;
+    pool.emplace_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, hi - lo); });
+  }
+  for (auto& th : pool) th.join();
+}
+std::mutex g_bounce_mu;
+char* g_bounce[2] = {nullptr, nullptr};
+
+bool page_locked(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice ||
+         a.type == hipMemoryTypeManaged;
+}
+
+int bounce_buffers() {
+  for (auto& b : g_bounce)
+    if (!b) HIP_TRY(hipHostMalloc((void**)&b, kBounceChunk, hipHostMallocDefault));
+  return kOk;
+}
+
+int bounce_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+  std::lock_guard<std::mutex> lock(g_bounce_mu);
+  if (int rc = bounce_buffers()) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (bytes + kBounceChunk - 1) / kBounceChunk;
+  auto len = [&](size_t i) { return i + 1 < n ? kBounceChunk : bytes - i * kBounceChunk; };
+  HIP_TRY(hipMemcpyAsync(g_bounce[0], src, len(0), hipMemcpyDeviceToHost, s));
+  for (size_t i = 0; i < n; ++i) {
+    HIP_TRY(hipStreamSynchronize(s));   // chunk i is in g_bounce[i & 1]
+    if (i + 1 < n)
+      HIP_TRY(hipMemcpyAsync(g_bounce[(i + 1) & 1], (const char*)src + (i + 1) * kBounceChunk,
+                             len(i + 1), hipMemcpyDeviceToHost, s));
+    host_copy((char*)dst + i * kBounceChunk, g_bounce[i & 1], len(i));
+  }
+  return kOk;
+}
+
+int bounce_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+  std::lock_guard<std::mutex> lock(g_bounce_mu);
+  if (int rc = bounce_buffers()) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (bytes + kBounceChunk - 1) / kBounceChunk;
+  for (size_t i = 0; i < n; ++i) {
+    const size_t l = i + 1 < n ? kBounceChunk : bytes - i * kBounceChunk;
+    if (i >= 2) HIP_TRY(hipStreamSynchronize(s));   // chunk i - 2 has left g_bounce[i & 1]
+    host_copy(g_bounce[i & 1], (const char*)src + i * kBounceChunk, l);
+    HIP_TRY(hipMemcpyAsync((char*)dst + i * kBounceChunk, g_bounce[i & 1], l,
+                           hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return kOk;
+}
+}  // namespace
+
+extern "C" {
+
 int dpf_hip_alloc(void** ptr, size_t bytes) {
   if (!ptr) return fail(kInvalidArgument, "ptr is NULL");
   *ptr = nullptr;
@@ -577,12 +680,30 @@ int dpf_hip_free(void* ptr) {
 }
 int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
   if (!bytes) return kOk;
+  if (bytes >= kBounceMin && !page_locked(src)) return bounce_h2d(dst, src, bytes, stream);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   return kOk;
 }
+int dpf_hip_host_alloc(void** ptr, size_t bytes) {
+  if (!ptr) return fail(kInvalidArgument, "ptr is NULL");
+  *ptr = nullptr;
+  if (bytes == 0) bytes = 1;
+  HIP_TRY(hipHostMalloc(ptr, bytes, hipHostMallocDefault));
+  return kOk;
+}
+int dpf_hip_host_free(void* ptr) {
+  if (ptr) HIP_TRY(hipHostFree(ptr));
+  return kOk;
+}
+int dpf_hip_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return kOk;
+  HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  return kOk;
+}
 int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
   if (!bytes) return kOk;
+  if (bytes >= kBounceMin && !page_locked(dst)) return bounce_d2h(dst, src, bytes, stream);
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   return kOk;
@@ -611,7 +732,8 @@ int dpf_hip_hash(int64_t n, const dpf_block* in, const dpf_aes_key* key, dpf_blo
   if (n < 0) return fail(kInvalidArgument, "n < 0");
   if (n == 0) return kOk;
   if (!in || !out || !key) return fail(kInvalidArgument, "NULL pointer");
-  hipLaunchKernelGGL(hash_kernel, dim3(grid_for(n)), dim3(kBlock), 0, (hipStream_t)stream, n,
+  const int blk = block_for(n);
+  hipLaunchKernelGGL(hash_kernel, dim3(grid_for(n, blk)), dim3(blk), 0, (hipStream_t)stream, n,
                      in, out, expand_key(key));
   HIP_TRY(hipGetLastError());
   return kOk;
@@ -650,7 +772,8 @@ int dpf_hip_eval_paths(int64_t num_seeds, int num_levels, const dpf_block* seeds
   p.ctrl_out = control_out;
   p.rkl = expand_key(key_left);
   p.rkd = xor_keys(p.rkl, expand_key(key_right));
-  hipLaunchKernelGGL(eval_paths_kernel, dim3(grid_for(num_seeds)), dim3(kBlock), 0, s, p);
+  const int blk = block_for(num_seeds);
+  hipLaunchKernelGGL(eval_paths_kernel, dim3(grid_for(num_seeds, blk)), dim3(blk), 0, s, p);
   HIP_TRY(hipGetLastError());
   return kOk;
 }

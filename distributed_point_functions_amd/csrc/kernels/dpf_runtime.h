@@ -19,7 +19,9 @@ int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
 
 int num_cus();                                 // compute units of the current device
-int grid_for(int64_t work_items);              // workgroups of kBlock threads, <= one per CU
+int block_for(int64_t work_items);             // threads per workgroup: kBlock, or fewer
+                                               // (multiple of 64) to spread a small launch over more CUs
+int grid_for(int64_t work_items, int block);   // workgroups of `block` threads, <= one per CU
 int validate_desc(const dpf_value_desc* d);    // kOk or the failure code
 int packed_size(const dpf_value_desc* d);      // bytes of one packed element
 bool fast_int(const dpf_value_desc* d);        // one plain/XOR integer leaf, direct, b == 1

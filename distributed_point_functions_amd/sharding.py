@@ -80,6 +80,8 @@ def all_gather_shares(packed):
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return packed.cpu().numpy().reshape(1, -1)
+    if packed.is_cuda and dist.get_backend() == "gloo":
+        packed = packed.cpu()   # gloo all-gathers host tensors only
     parts = [torch.empty_like(packed) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, packed.contiguous())
     return np.stack([p.cpu().numpy().reshape(-1) for p in parts])

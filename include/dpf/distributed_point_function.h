@@ -150,9 +150,23 @@ class DistributedPointFunction {
   StatusOr<std::vector<T>> EvaluateUntil(int hierarchy_level, Span<const uint128> prefixes,
                                          EvaluationContext& ctx) const {
     ValueType t = ToValueType<T>();
-    StatusOr<std::vector<uint8_t>> packed = EvaluateUntilPacked(hierarchy_level, prefixes, ctx, &t);
-    if (!packed.ok()) return packed.status();
-    return Unpack<T>(hierarchy_level, *packed);
+    if constexpr (dpf_internal::kPackedIsMemoryImage<T>) {
+      // The packed elements are T's memory image: copy them from the device
+      // straight into the result.
+      std::vector<T> out;
+      const HostSink sink = [&out](size_t bytes) -> void* {
+        out = dpf_internal::MakeOutputVector<T>(static_cast<int64_t>(bytes / sizeof(T)));
+        return out.data();
+      };
+      Status status = EvaluateUntilToHost(hierarchy_level, prefixes, ctx, &t, sink);
+      if (!status.ok()) return status;
+      return out;
+    } else {
+      StatusOr<std::vector<uint8_t>> packed =
+          EvaluateUntilPacked(hierarchy_level, prefixes, ctx, &t);
+      if (!packed.ok()) return packed.status();
+      return Unpack<T>(hierarchy_level, *packed);
+    }
   }
 
   template <typename T>
@@ -186,6 +200,12 @@ class DistributedPointFunction {
 
   // ---- type-erased core (packed elements) --------------------------------
   // `requested_type` (may be null) plays the role of T in the templates.
+  // A HostSink is called once with the output size in bytes and returns where
+  // the packed output is to be copied.
+  using HostSink = std::function<void*(size_t bytes)>;
+  Status EvaluateUntilToHost(int hierarchy_level, Span<const uint128> prefixes,
+                             EvaluationContext& ctx, const ValueType* requested_type,
+                             const HostSink& sink) const;
   StatusOr<std::vector<uint8_t>> EvaluateUntilPacked(int hierarchy_level,
                                                      Span<const uint128> prefixes,
                                                      EvaluationContext& ctx,
@@ -325,7 +345,7 @@ class DistributedPointFunction {
   Status EvaluateUntilCore(int hierarchy_level, Span<const uint128> prefixes,
                            EvaluationContext& ctx, const ValueType* requested_type,
                            void* device_out, int64_t capacity_bytes, void* stream,
-                           std::vector<uint8_t>* host_out, int64_t* num_elements) const;
+                           const HostSink* host_out, int64_t* num_elements) const;
   // ComputePartialEvaluations (cc:351-453), path walk on the GPU.
   // `before_device` (may be empty) runs after the host-side lookups and before
   // any device work, so host validation errors never leave work in flight.

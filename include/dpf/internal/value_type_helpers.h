@@ -11,6 +11,7 @@
 #define DPF_INTERNAL_VALUE_TYPE_HELPERS_H_
 
 #include <cstring>
+#include <functional>
 #include <string>
 #include <type_traits>
 #include <utility>
@@ -207,25 +208,50 @@ StatusOr<T> FromValueImpl(const Value& value) {
   return ValueTypeHelper<T>::FromLeaves(leaves->data());
 }
 
+// Plain unsigned integers: the packed image of n elements IS the array of T.
+template <typename T>
+constexpr bool kPackedIsMemoryImage =
+    (std::is_integral_v<T> && std::is_unsigned_v<T> && !std::is_same_v<T, bool>) ||
+    std::is_same_v<T, uint128>;
+
+// Asks the kernel for transparent huge pages on [p, p + bytes) before it is
+// first touched: a fresh 128 MiB output vector costs ~22 ms of 4 KiB page
+// faults on the GPU box's host, ~7 ms with 2 MiB pages.  No-op below 4 MiB.
+void AdviseHugePages(void* p, size_t bytes);
+
+// A value-initialised std::vector<T> of n elements whose storage was advised
+// onto huge pages before the initialisation touched it.
+template <typename T>
+std::vector<T> MakeOutputVector(int64_t n) {
+  std::vector<T> out;
+  out.reserve(n);
+  AdviseHugePages(out.data(), static_cast<size_t>(n) * sizeof(T));
+  out.resize(n);
+  return out;
+}
+
+// fn(lo, hi) over [0, n) in chunks of at least `grain`, on up to 16 host threads.
+void ParallelRanges(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn);
+
 // Unpacks n packed elements of T.
 template <typename T>
 std::vector<T> UnpackElements(const FlatValueType& flat, const uint8_t* data, int64_t n) {
-  // Plain unsigned integers: the packed image IS the array of T.
-  if constexpr ((std::is_integral_v<T> && std::is_unsigned_v<T>) || std::is_same_v<T, uint128>) {
+  if constexpr (kPackedIsMemoryImage<T>) {
     if (flat.leaves.size() == 1 && flat.packed_size == static_cast<int>(sizeof(T)) &&
         flat.leaves[0].bits == static_cast<int>(8 * sizeof(T)) && flat.leaves[0].kind == kLeafInt) {
-      std::vector<T> out(n);
+      std::vector<T> out = MakeOutputVector<T>(n);
       if (n) std::memcpy(out.data(), data, n * sizeof(T));
       return out;
     }
   }
-  std::vector<T> out;
-  out.reserve(n);
-  std::vector<uint128> leaves(flat.leaves.size());
-  for (int64_t i = 0; i < n; ++i) {
-    UnpackLeaves(flat, data + i * flat.packed_size, leaves.data());
-    out.push_back(ValueTypeHelper<T>::FromLeaves(leaves.data()));
-  }
+  std::vector<T> out = MakeOutputVector<T>(n);
+  ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
+    std::vector<uint128> leaves(flat.leaves.size());
+    for (int64_t i = lo; i < hi; ++i) {
+      UnpackLeaves(flat, data + i * flat.packed_size, leaves.data());
+      out[i] = ValueTypeHelper<T>::FromLeaves(leaves.data());
+    }
+  });
   return out;
 }
 

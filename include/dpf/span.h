@@ -26,6 +26,12 @@ class Span {
             typename = std::enable_if_t<std::is_convertible_v<
                 std::remove_pointer_t<decltype(std::declval<C&>().data())> (*)[], T (*)[]>>>
   constexpr Span(C& c) : data_(c.data()), size_(c.size()) {}  // NOLINT
+  // Read-only spans also bind const containers and temporaries (absl::Span<const T>).
+  template <typename C, typename U = T, typename = std::enable_if_t<std::is_const_v<U>>,
+            typename = decltype(std::declval<const C&>().data()),
+            typename = std::enable_if_t<std::is_convertible_v<
+                std::remove_pointer_t<decltype(std::declval<const C&>().data())> (*)[], T (*)[]>>>
+  constexpr Span(const C& c) : data_(c.data()), size_(c.size()) {}  // NOLINT
   template <typename U = T, typename = std::enable_if_t<std::is_const_v<U>>>
   Span(std::initializer_list<value_type> il) : data_(il.begin()), size_(il.size()) {}  // NOLINT
 

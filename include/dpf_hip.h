@@ -83,6 +83,12 @@ int dpf_hip_set_device(int device);
 int dpf_hip_alloc(void** ptr, size_t bytes);
 int dpf_hip_free(void* ptr);
 int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+/* Page-locked host memory, and an H2D copy that does not wait: `src` must be
+ * page-locked (dpf_hip_host_alloc) and stay unchanged until `stream` has run
+ * the copy.  The host API stages its small per-call uploads this way. */
+int dpf_hip_host_alloc(void** ptr, size_t bytes);
+int dpf_hip_host_free(void* ptr);
+int dpf_hip_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memset(void* dst, int value, size_t bytes, void* stream);
