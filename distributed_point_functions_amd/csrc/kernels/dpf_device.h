@@ -67,11 +67,16 @@ struct LdsImage {
 // Table image: 256-byte rows.  Row e of the low 64 KiB = [T0[e] x 32 copies |
 // T1[e] x 32 copies], of the high 64 KiB = [T2[e] x 32 | T3[e] x 32].  Lane l
 // reads copy (l & 31), so every ds_read_b32 of a wave is bank-conflict-free.
+// Filled 16 bytes (4 copies) per store: 8192 ds_write_b128 per workgroup, so a
+// small workgroup (block_for) fills its tables in a few microseconds.
 __device__ __forceinline__ void fill_tables(uint32_t* tab) {
-  for (int i = threadIdx.x; i < kTabWords; i += blockDim.x) {
-    int t = 2 * (i >> 14) + ((i >> 5) & 1), e = (i >> 6) & 255;
-    uint32_t v = c_t0.v[e];
-    tab[i] = t == 0 ? v : ((v << (8 * t)) | (v >> (32 - 8 * t)));
+  for (int q = threadIdx.x; q < kTabWords / 4; q += blockDim.x) {
+    // q = (entry e, table t, quad k): words [half * 16384 + e * 64 + (t & 1) * 32 + 4k, +4)
+    const int e = q >> 5, t = (q >> 3) & 3, k = q & 7;
+    const uint32_t v0 = c_t0.v[e];
+    const uint32_t v = t == 0 ? v0 : ((v0 << (8 * t)) | (v0 >> (32 - 8 * t)));
+    *reinterpret_cast<uint4*>(tab + (t >> 1) * 16384 + e * 64 + (t & 1) * 32 + 4 * k) =
+        make_uint4(v, v, v, v);
   }
 }
 

@@ -302,9 +302,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) 
       for (int j = 0; j < L; ++j) {
         const uint32_t b0 = path_bit(path0, L - 1 - j + bb), b1 = path_bit(path1, L - 1 - j + bb);
         const dpf_block c = cws[j];
+        const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
         const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
                                     (uint32_t)(c.high >> 32));
-        const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
         path_step2(lk, p.rkl, p.rkd, s0, t0, b0, s1, t1, b1, cs, cctl);
       }
       const dpf_block* vcw = p.vcw + k * p.vcw_stride;
@@ -799,8 +799,9 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
   // Choose the depth-first subtree depth S and the per-item walk depth k0.
   const int64_t threads = (int64_t)num_cus() * kBlock;
   int S = num_levels < kSMax ? num_levels : kSMax;
-  const int s_min = num_levels < 4 ? num_levels : 4;
-  while (S > s_min && (num_starts << (num_levels - S)) < threads) --S;
+  // Small trees: shallow subtrees and more items, so that a launch far below
+  // one full workgroup per CU is not serialised on a few lanes' DFS.
+  while (S > 1 && (num_starts << (num_levels - S)) < threads) --S;
   ExpandParams p;
   p.num_levels = num_levels;
   p.S = S;
