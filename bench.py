@@ -186,7 +186,12 @@ def profiled_traffic(leaves_per_launch: int):
             continue
         if (s.get("leaves_per_launch") == leaves_per_launch and "hbm_traffic_bytes" in s
                 and "expand_kernel" in s.get("kernel", "")):
-            best = (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT))
+            best = (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT),
+                    {"valu_lane_ops_per_aes": s.get("valu_lane_ops_per_aes"),
+                     "lds_lane_ops_per_aes": s.get("lds_lane_ops_per_aes"),
+                     "sustained_clock_ghz": s.get("effective_clock_ghz"),
+                     "clk_per_aes_per_cu": s.get("clk_per_aes_per_cu"),
+                     "profiled_launch_ms": s.get("avg_ns", 0) / 1e6})
     return best
 
 
@@ -320,6 +325,7 @@ def main():
                          "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
                          "traffic": tr[0] if tr else None,
                          "traffic_source": tr[1] if tr else None,
+                         "pmc": tr[2] if tr else None,
                          "kernel": KERNEL.replace("64", str(bits)), "launch_ms": kern_ms_max,
                          "algorithmic_aes_per_launch": aes_per_launch,
                          "algorithmic_bytes_per_launch": bytes_per_launch},
