@@ -34,20 +34,16 @@ void SetToZero(Value& value) {
   }
 }
 
-// A device allocation released on scope exit.
-struct DeviceMem {
-  void* p = nullptr;
-  ~DeviceMem() {
-    if (p) dpf_hip_free(p);
-  }
-  Status Alloc(size_t bytes) { return FromHip(dpf_hip_alloc(&p, std::max<size_t>(bytes, 16))); }
-};
 
 }  // namespace
 
 DistributedComparisonFunction::DistributedComparisonFunction(
     DcfParameters parameters, std::unique_ptr<DistributedPointFunction> dpf)
-    : parameters_(std::move(parameters)), dpf_(std::move(dpf)) {}
+    : parameters_(std::move(parameters)),
+      dpf_(std::move(dpf)),
+      scratch_(new dpf_internal::DeviceScratch()) {}
+
+DistributedComparisonFunction::~DistributedComparisonFunction() = default;
 
 StatusOr<std::unique_ptr<DistributedComparisonFunction>> DistributedComparisonFunction::Create(
     const DcfParameters& parameters) {
@@ -134,21 +130,36 @@ StatusOr<int64_t> DistributedComparisonFunction::EvaluateBatchToDevice(
       return InvalidArgumentError(
           "`evaluation_points[0]` larger than the domain size at hierarchy level 0");
   }
-  std::vector<int32_t> depth(n), blocks(n);
   std::vector<const dpf_block*> vcw(n);
+  for (int i = 0; i < n; ++i) vcw[i] = keys.value_correction(i);
+  DPF_RETURN_IF_ERROR(Launch(keys.num_keys(), points_per_key, shared_points, keys.seed(),
+                             keys.party(), static_cast<const dpf_block*>(device_points),
+                             keys.cw_seed(), keys.cw_left(), keys.cw_right(), keys.num_levels(),
+                             vcw, device_out, stream));
+  return total;
+}
+
+Status DistributedComparisonFunction::Launch(int64_t num_keys, int64_t points_per_key,
+                                             bool shared_points, const dpf_block* seed,
+                                             const uint8_t* party, const dpf_block* points,
+                                             const dpf_block* cw_seed, const uint8_t* cw_left,
+                                             const uint8_t* cw_right, int cw_stride,
+                                             const std::vector<const dpf_block*>& vcw,
+                                             void* device_out, void* stream) const {
+  const int n = parameters_.parameters().log_domain_size();
+  const auto& f = dpf_->flat_value_type(0);
+  std::vector<int32_t> depth(n), blocks(n);
   for (int i = 0; i < n; ++i) {
     depth[i] = dpf_->hierarchy_to_tree()[i];
     blocks[i] = dpf_->blocks_needed(i);
-    vcw[i] = keys.value_correction(i);
   }
   const dpf_value_desc desc = MakeDesc(f, blocks[0]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   HIP_RETURN_IF_ERROR(dpf_hip_dcf_eval_batch(
-      keys.num_keys(), points_per_key, shared_points ? 1 : 0, n, depth.data(), blocks.data(),
-      keys.seed(), keys.party(), static_cast<const dpf_block*>(device_points), keys.cw_seed(),
-      keys.cw_left(), keys.cw_right(), keys.num_levels(), vcw.data(), &kl, &kr, &kv, &desc,
-      device_out, stream));
-  return total;
+      num_keys, points_per_key, shared_points ? 1 : 0, n, depth.data(), blocks.data(), seed, party,
+      points, cw_seed, cw_left, cw_right, cw_stride, vcw.data(), &kl, &kr, &kv, &desc, device_out,
+      stream));
+  return OkStatus();
 }
 
 StatusOr<std::vector<uint8_t>> DistributedComparisonFunction::EvaluateByLevels(
@@ -194,18 +205,39 @@ StatusOr<std::vector<uint8_t>> DistributedComparisonFunction::EvaluatePacked(
   if (xs.empty()) return std::vector<uint8_t>{};
   const auto& f = dpf_->flat_value_type(0);
   if (f.leaves.size() > 4) return EvaluateByLevels(key, xs);
-  DPF_ASSIGN_OR_RETURN(std::unique_ptr<DeviceKeyBatch> dev, DeviceKeyBatch::Upload(batch, nullptr));
+  // One key: its arrays and the points go through the reused scratch buffers
+  // (staged, no per-call allocation), then one launch and one copy back.
+  auto* s = scratch_.get();
   const int64_t m = static_cast<int64_t>(xs.size());
   std::vector<dpf_block> pts(m);
   for (int64_t i = 0; i < m; ++i) pts[i] = ToBlock(xs[i]);
-  DeviceMem dpts, dout;
-  DPF_RETURN_IF_ERROR(dpts.Alloc(m * sizeof(dpf_block)));
-  DPF_RETURN_IF_ERROR(dout.Alloc(m * f.packed_size));
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(dpts.p, pts.data(), m * sizeof(dpf_block), nullptr));
-  DPF_RETURN_IF_ERROR(
-      EvaluateBatchToDevice(*dev, dpts.p, m, false, dout.p, m * f.packed_size, nullptr).status());
+  const int L = batch.num_levels;
+  std::vector<dpf_block> vcw_all;
+  std::vector<size_t> vcw_off(n);
+  for (int i = 0; i < n; ++i) {
+    vcw_off[i] = vcw_all.size();
+    vcw_all.insert(vcw_all.end(), batch.value_correction[i].begin(),
+                   batch.value_correction[i].end());
+  }
+  dpf_internal::PackedUploads& up = s->packed;
+  DPF_RETURN_IF_ERROR(up.Reset());
+  const size_t o_seed = up.Add(batch.seed.data(), 1);
+  const size_t o_party = up.Add(batch.party.data(), 1);
+  const size_t o_cws = up.Add(batch.cw_seed.data(), L);
+  const size_t o_cwl = up.Add(batch.cw_left.data(), L);
+  const size_t o_cwr = up.Add(batch.cw_right.data(), L);
+  const size_t o_vcw = up.Add(vcw_all.data(), vcw_all.size());
+  const size_t o_pts = up.Add(pts.data(), pts.size());
+  DPF_RETURN_IF_ERROR(up.Commit(nullptr));
+  DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(m) * f.packed_size));
+  std::vector<const dpf_block*> vcw(n);
+  for (int i = 0; i < n; ++i) vcw[i] = up.Ptr<dpf_block>(o_vcw) + vcw_off[i];
+  DPF_RETURN_IF_ERROR(Launch(1, m, false, up.Ptr<dpf_block>(o_seed), up.Ptr<uint8_t>(o_party),
+                             up.Ptr<dpf_block>(o_pts), up.Ptr<dpf_block>(o_cws),
+                             up.Ptr<uint8_t>(o_cwl), up.Ptr<uint8_t>(o_cwr), L, vcw,
+                             s->out.get(), nullptr));
   std::vector<uint8_t> out(m * f.packed_size);
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), dout.p, out.size(), nullptr));
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
   return out;
 }
 

@@ -21,6 +21,7 @@
 namespace distributed_point_functions {
 
 using dpf_internal::AesKey;
+using dpf_internal::PackedUploads;
 using dpf_internal::FromBlock;
 using dpf_internal::FromHip;
 using dpf_internal::FromProtoBlock;
@@ -297,6 +298,27 @@ Status UploadCorrectionWords(const DpfKey& key, int start, int stop,
   DPF_RETURN_IF_ERROR(s->Upload(s->cw_left, cl.data(), cl.size(), stream));
   return s->Upload(s->cw_right, cr.data(), cr.size(), stream);
 }
+
+// Correction words [start, stop) of `key` added to a packed upload.
+struct PackedCws {
+  size_t seed, left, right;
+};
+PackedCws AddCorrectionWords(const DpfKey& key, int start, int stop, PackedUploads& up) {
+  const int L = stop - start;
+  std::vector<dpf_block> seeds(std::max(L, 1));
+  std::vector<uint8_t> cl(std::max(L, 1)), cr(std::max(L, 1));
+  for (int j = 0; j < L; ++j) {
+    const CorrectionWord& cw = key.correction_words(start + j);
+    seeds[j] = ToBlock(FromProtoBlock(cw.seed()));
+    cl[j] = cw.control_left();
+    cr[j] = cw.control_right();
+  }
+  PackedCws o;
+  o.seed = up.Add(seeds.data(), seeds.size());
+  o.left = up.Add(cl.data(), cl.size());
+  o.right = up.Add(cr.data(), cr.size());
+  return o;
+}
 }  // namespace
 
 Status DistributedPointFunction::ComputePartialEvaluations(
@@ -495,15 +517,16 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   };
   DeviceStart start;
   int start_level = 0;
+  PackedUploads& up = s->packed;
+  DPF_RETURN_IF_ERROR(up.Reset());
+  size_t o_root = 0, o_party = 0;
   if (tree_indices.empty()) {
     DPF_RETURN_IF_ERROR(parse_vcw());
-    dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
-    uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
-    DPF_RETURN_IF_ERROR(s->Upload(s->start_seed, &root, 1, stream));
-    DPF_RETURN_IF_ERROR(s->Upload(s->start_ctrl, &party, 1, stream));
+    const dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+    const uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
+    o_root = up.Add(&root, 1);
+    o_party = up.Add(&party, 1);
     start.n = 1;
-    start.seeds = s->start_seed.as<dpf_block>();
-    start.ctrl = s->start_ctrl.as<uint8_t>();
   } else {
     const bool update_ctx = hierarchy_level < H - 1;
     DPF_RETURN_IF_ERROR(ComputePartialEvaluations(MakeConstSpan(tree_indices),
@@ -525,8 +548,13 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
 
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw_blocks.data(), vcw_blocks.size(), stream));
-  DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), start_level, stop_level, s, stream));
+  const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());
+  const PackedCws o_cw = AddCorrectionWords(ctx.key(), start_level, stop_level, up);
+  DPF_RETURN_IF_ERROR(up.Commit(stream));
+  if (tree_indices.empty()) {
+    start.seeds = up.Ptr<dpf_block>(o_root);
+    start.ctrl = up.Ptr<uint8_t>(o_party);
+  }
 
   // Is the gather (h:822-835) the identity?  Yes when every prefix maps to its
   // own tree index in order and covers the whole expanded block range.
@@ -548,10 +576,10 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   }
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
-  HIP_RETURN_IF_ERROR(dpf_hip_expand(start.n, start.seeds, start.ctrl, L, s->cw_seed.as<dpf_block>(),
-                                     s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr, &kv,
-                                     &desc, cepb, s->vcw.as<dpf_block>(), ctx.key().party() & 1,
-                                     expand_out, stream));
+  HIP_RETURN_IF_ERROR(dpf_hip_expand(start.n, start.seeds, start.ctrl, L, up.Ptr<dpf_block>(o_cw.seed),
+                                     up.Ptr<uint8_t>(o_cw.left), up.Ptr<uint8_t>(o_cw.right), &kl, &kr,
+                                     &kv, &desc, cepb, up.Ptr<dpf_block>(o_vcw),
+                                     ctx.key().party() & 1, expand_out, stream));
   void* result = expand_out;
   if (!identity) {
     std::vector<int64_t> offsets(num_prefixes);
@@ -718,26 +746,31 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
                                                   nullptr));
     start_level = stop_level;
   }
+  // All argument arrays in one packed upload (PackedUploads).
   std::vector<dpf_block> paths(n);
   for (int64_t i = 0; i < n; ++i) paths[i] = ToBlock(tree_indices[i]);
-  DPF_RETURN_IF_ERROR(s->Upload(s->paths, paths.data(), paths.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->block_index, block_index.data(), block_index.size()));
-  DPF_RETURN_IF_ERROR(UploadCorrectionWords(key, start_level, stop_level, s, nullptr));
+  const int L = stop_level - start_level;
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw_blocks.data(), vcw_blocks.size()));
-  dpf_block root = ToBlock(FromProtoBlock(key.seed()));
-  uint8_t party = static_cast<uint8_t>(key.party() & 1);
-  DPF_RETURN_IF_ERROR(s->Upload(s->key_seed, &root, 1));
-  DPF_RETURN_IF_ERROR(s->Upload(s->party, &party, 1));
+  const dpf_block root = ToBlock(FromProtoBlock(key.seed()));
+  const uint8_t party = static_cast<uint8_t>(key.party() & 1);
+  PackedUploads& up = s->packed;
+  DPF_RETURN_IF_ERROR(up.Reset());
+  const size_t o_paths = up.Add(paths.data(), paths.size());
+  const size_t o_bi = up.Add(block_index.data(), block_index.size());
+  const PackedCws o_cw = AddCorrectionWords(key, start_level, stop_level, up);
+  const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());
+  const size_t o_root = up.Add(&root, 1);
+  const size_t o_party = up.Add(&party, 1);
+  DPF_RETURN_IF_ERROR(up.Commit(nullptr));
   DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   HIP_RETURN_IF_ERROR(dpf_hip_eval_points(
-      n, n, stop_level - start_level, s->key_seed.as<dpf_block>(), s->party.as<uint8_t>(),
-      ctx ? start.seeds : nullptr, ctx ? start.ctrl : nullptr, s->paths.as<dpf_block>(),
-      s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
-      s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc, s->vcw.as<dpf_block>(), s->out.get(),
+      n, n, L, up.Ptr<dpf_block>(o_root), up.Ptr<uint8_t>(o_party),
+      ctx ? start.seeds : nullptr, ctx ? start.ctrl : nullptr, up.Ptr<dpf_block>(o_paths),
+      up.Ptr<int32_t>(o_bi), up.Ptr<dpf_block>(o_cw.seed), up.Ptr<uint8_t>(o_cw.left),
+      up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), s->out.get(),
       nullptr));
   std::vector<uint8_t> out =
       dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(n) * f.packed_size);

@@ -20,6 +20,10 @@
 
 namespace distributed_point_functions {
 
+namespace dpf_internal {
+class DeviceScratch;
+}
+
 class DistributedComparisonFunction {
  public:
   static StatusOr<std::unique_ptr<DistributedComparisonFunction>> Create(
@@ -47,6 +51,7 @@ class DistributedComparisonFunction {
 
   DistributedComparisonFunction(const DistributedComparisonFunction&) = delete;
   DistributedComparisonFunction& operator=(const DistributedComparisonFunction&) = delete;
+  ~DistributedComparisonFunction();
 
   // ---- MI355X extensions ---------------------------------------------------
   // GenerateKeys with caller-supplied root seeds (reproducible fixtures).
@@ -77,8 +82,17 @@ class DistributedComparisonFunction {
   // does not take (more than 4 tuple leaves).
   StatusOr<std::vector<uint8_t>> EvaluateByLevels(const DcfKey& key, Span<const uint128> xs);
 
+  // The kernel launch shared by the device-batch and host entry points.
+  Status Launch(int64_t num_keys, int64_t points_per_key, bool shared_points,
+                const dpf_block* seed, const uint8_t* party, const dpf_block* points,
+                const dpf_block* cw_seed, const uint8_t* cw_left, const uint8_t* cw_right,
+                int cw_stride, const std::vector<const dpf_block*>& vcw, void* device_out,
+                void* stream) const;
+
   const DcfParameters parameters_;
   const std::unique_ptr<DistributedPointFunction> dpf_;
+  // Reused device buffers and staged uploads of the host entry points.
+  const std::unique_ptr<dpf_internal::DeviceScratch> scratch_;
 };
 
 }  // namespace distributed_point_functions

@@ -1,5 +1,6 @@
 // dpf_benchmark.cc -- the reference's benchmark suite
-// (dpf/distributed_point_function_benchmark.cc) restated against this build's
+// (dpf/distributed_point_function_benchmark.cc, and BM_EvaluateDcf of
+// dcf/distributed_comparison_function_benchmark.cc) restated against this build's
 // drop-in C++ API: same benchmark names, value types and argument ranges, the
 // same API calls in the timed loops, so a user of the reference can compare
 // numbers case by case.  Evaluation runs on the GPU through the C ABI; key
@@ -27,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "dcf/distributed_comparison_function.h"
 #include "dpf/distributed_point_function.h"
 #include "dpf/int_mod_n.h"
 #include "dpf/tuple.h"
@@ -324,6 +326,34 @@ void BatchEvaluation(Runner& r) {
   }
 }
 
+// BM_EvaluateDcf<T>/log: one Evaluate<T>(key, x) per iteration, x counting up
+// (dcf/distributed_comparison_function_benchmark.cc:24-54), beta = 42.  Each
+// call is one GPU launch, so this measures the per-call latency; the batched
+// API (EvaluateBatchToDevice, bench.py --workload dcf) is the throughput path.
+template <typename T>
+void EvaluateDcf(Runner& r, const std::string& tname) {
+  for (int log = 2; log <= 24; log += 2) {
+    const std::string name = "BM_EvaluateDcf<" + tname + ">/" + std::to_string(log);
+    if (!std::regex_search(name, r.filter)) continue;
+    dpf::DcfParameters p;
+    *p.mutable_parameters()->mutable_value_type() = dpf::ToValueType<T>();
+    p.mutable_parameters()->set_log_domain_size(log);
+    auto f = Must(dpf::DistributedComparisonFunction::Create(p), "DCF Create");
+    const uint128 mask = (uint128{1} << log) - 1;
+    std::mt19937_64 rng(log);
+    const uint128 alpha = dpf::MakeUint128(rng(), rng()) & mask;
+    auto keys = Must(f->GenerateKeys(alpha, T(42)), "DCF GenerateKeys");
+    uint128 x = 0;
+    r.Run(name, [&](int64_t n) {
+      for (int64_t it = 0; it < n; ++it) {
+        T v = Must(f->template Evaluate<T>(keys.first, x), "DCF Evaluate");
+        g_sink<T> = static_cast<size_t>(v == T{});
+        x = (x + 1) & mask;
+      }
+    });
+  }
+}
+
 using MyIntModN = IntModN<uint32_t, 4294967291u>;                 // 2^32 - 5
 using MyIntModN64 = IntModN<uint64_t, 18446744073709551557ull>;   // 2^64 - 59
 
@@ -377,6 +407,11 @@ int main(int argc, char** argv) {
   KeyGeneration<false>(r);
   HeavyHitters(r);
   BatchEvaluation(r);
+  EvaluateDcf<uint8_t>(r, "uint8_t");
+  EvaluateDcf<uint16_t>(r, "uint16_t");
+  EvaluateDcf<uint32_t>(r, "uint32_t");
+  EvaluateDcf<uint64_t>(r, "uint64_t");
+  EvaluateDcf<uint128>(r, "uint128");
   if (!json.empty()) {
     std::ofstream o(json);
     o << "[\n";
