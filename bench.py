@@ -106,6 +106,19 @@ def _int_of(v) -> int:
 CPU_THREADS = min(16, os.cpu_count() or 1)   # the GPU box's CPU share is 16 per GPU
 
 
+def host_cpu() -> dict:
+    """CPU model and logical CPU count of the host the baseline ran on."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "threads_used": CPU_THREADS}
+
+
 def run_cpu_pool(work, items, threads: int = CPU_THREADS, budget_s: float = 15.0):
     """Runs work(item) -> units over `items` on `threads` host threads (the
     oracle's C calls release the GIL), submitting new items only while the
@@ -166,7 +179,13 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
         return O.hash_correct(("int", bits), es, ec, 1, P.cepb(0), vcw, k["party"]).shape[0]
 
     leaves, dt, done = run_cpu_pool(work, range(n_sub), budget_s=20.0)
+    # SURVEY.md 8d also asks for the single-threaded rate (the reference is
+    # single-threaded): a 4 s sample on one thread.
+    leaves1, dt1, done1 = run_cpu_pool(work, range(n_sub), threads=1, budget_s=4.0)
     return {"value": leaves / dt, "unit": "leaves/s", "cores": CPU_THREADS, "kind": "port",
+            "single_thread_value": leaves1 / dt1,
+            "single_thread_sample": f"{done1} subtrees of 2^18 outputs, {dt1:.1f} s on 1 thread",
+            "host": host_cpu(),
             "sample": f"{done} of the {n_sub} subtrees of 2^18 uint{bits} outputs of the benchmark "
                       f"key (2^{log_domain} domain): EvaluateSeeds to each subtree root, then "
                       f"ExpandSeeds+HashExpandedSeeds+correction (oracle over OpenSSL AES-NI); "
@@ -371,7 +390,7 @@ def cpu_baseline_points(dpf, batch, points_fn, keys: int, ppk: int):
         return O.evaluate_at(P, okey, 0, points_fn(k)).shape[0]
 
     n, dt, done = run_cpu_pool(work, range(keys), budget_s=15.0)
-    return {"value": n / dt, "unit": "points/s", "cores": CPU_THREADS, "kind": "port",
+    return {"value": n / dt, "unit": "points/s", "cores": CPU_THREADS, "kind": "port", "host": host_cpu(),
             "sample": f"{done} keys x {ppk} points of the benchmark batch (log 128, uint64): "
                       f"EvaluateSeeds over 127 levels + value hash + correction (oracle over "
                       f"OpenSSL AES-NI); {dt:.1f} s wall on {CPU_THREADS} host threads",
@@ -815,7 +834,7 @@ def main_dcf(args):
 
             evals, dt, done = run_cpu_pool(work, range(nk), budget_s=10.0)
             res["cpu_baseline"] = {
-                "value": evals / dt, "unit": "evals/s", "cores": CPU_THREADS, "kind": "port",
+                "value": evals / dt, "unit": "evals/s", "cores": CPU_THREADS, "kind": "port", "host": host_cpu(),
                 "sample": f"{done} keys x 64 points: the reference's Evaluate (one EvaluateAt "
                           f"per level, h:83-105) on the oracle (keygen included), {dt:.1f} s "
                           f"wall on {CPU_THREADS} host threads"}
@@ -855,7 +874,7 @@ def cpu_baseline_heavy_hitters(logs, record, alphas, seeds, top_k, budget_s=15.0
         return sum(O.evaluate_until(P, h, pre, ctx).shape[0] for h, pre in enumerate(plan))
 
     outs, dt, done = run_cpu_pool(work, range(n_sample), budget_s=budget_s)
-    return {"value": outs / dt, "unit": "prefix evals/s", "cores": CPU_THREADS, "kind": "port",
+    return {"value": outs / dt, "unit": "prefix evals/s", "cores": CPU_THREADS, "kind": "port", "host": host_cpu(),
             "sample": f"{done} clients x all {len(logs)} levels of server 0 at the GPU run's "
                       f"candidates (EvaluateUntil per key, oracle over OpenSSL AES-NI); "
                       f"{dt:.1f} s wall on {CPU_THREADS} host threads"}
