@@ -133,16 +133,17 @@ def build_oracle(force=False):
 
 
 def build_tools(force=False):
-    """C++ programs written against the drop-in API (tools/*.cc): the
-    reference's benchmark suite restated (dpf_benchmark)."""
-    src = os.path.join(ROOT, "tools", "dpf_benchmark.cc")
-    out = os.path.join(LIBDIR, "dpf_benchmark")
+    """C++ programs written against the drop-in API: the reference's benchmark
+    suite restated (tools/dpf_benchmark.cc) and the C++ template tests
+    (tests/cpp/dpf_api_test.cc)."""
     hdrs = _files(os.path.join(INCLUDE), (".h",))
-    if force or _stale(out, [src, os.path.join(LIBDIR, "libdpf.so")] + hdrs):
-        cxx = os.environ.get("CXX", "g++")
-        _run([cxx, "-O2", "-std=c++20", "-Wall", f"-I{INCLUDE}", src, "-o", out, f"-L{LIBDIR}",
-              "-ldpf", "-ldpf_hip", "-Wl,-rpath,$ORIGIN"])
-    return out
+    cxx = os.environ.get("CXX", "g++")
+    for src, name in ((os.path.join(ROOT, "tools", "dpf_benchmark.cc"), "dpf_benchmark"),
+                      (os.path.join(ROOT, "tests", "cpp", "dpf_api_test.cc"), "dpf_api_test")):
+        out = os.path.join(LIBDIR, name)
+        if force or _stale(out, [src, os.path.join(LIBDIR, "libdpf.so")] + hdrs):
+            _run([cxx, "-O2", "-std=c++20", "-Wall", f"-I{INCLUDE}", src, "-o", out,
+                  f"-L{LIBDIR}", "-ldpf", "-ldpf_hip", "-Wl,-rpath,$ORIGIN"])
 
 
 def build_all(force=False):
