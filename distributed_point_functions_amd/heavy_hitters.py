@@ -18,8 +18,9 @@ identically on every rank and both servers (the threshold step of the
 two-server protocol, here run in one process).
 
 Keys are split across ranks by client (sharding.key_range); each rank sums
-over its own clients on the device and the per-rank sums are all-gathered and
-group-summed (sharding.aggregate_shares) -- the only data-path exchange,
+over its own clients on the device and the per-rank sums are combined by one
+all_reduce(SUM) of the widened IntModN32 leaves, reduced mod N on every rank
+(sharding.aggregate_shares) -- the only data-path exchange,
 <= top_k * 4 elements of 8 bytes per level and server.
 """
 from __future__ import annotations

@@ -60,10 +60,14 @@ def max_over_ranks(value: float, device=None) -> float:
 # into `world` contiguous row ranges (DeviceKeyBatch.upload(begin, end)).
 # Per-key outputs stay on their rank; the aggregation variant reduces over the
 # rank's keys on the device (dpf_hip_eval_points_sum) and then combines the
-# per-rank partial sums -- the only data-path exchange: one all_gather of
-# num_points packed elements (a few KiB over xGMI) followed by the group sum
-# (integers mod 2^bits, IntModN mod N, XOR) on every rank.  All-gather rather
-# than all_reduce(SUM) because the group is not always the integers mod 2^64.
+# per-rank partial sums -- the only data-path exchange, a few KiB over xGMI:
+# * value types whose leaves are integers of <= 64 bits or IntModN with
+#   N <= 2^32 (uint64 of config 4, Tuple<IntModN32, IntModN32> of config 5b):
+#   each leaf widened to int64, ONE all_reduce(SUM) (RCCL), then reduced mod
+#   2^bits or mod N locally (SURVEY.md 8e; at most 2^31 ranks keep an IntModN32
+#   sum inside int64);
+# * anything else (uint128, IntModN over 64-bit bases, XorWrapper): one
+#   all_gather of the packed sums and the group sum on every rank.
 
 def key_range(num_keys: int, world: int, rank: int) -> tuple:
     """[begin, end) of the keys rank `rank` owns (balanced contiguous split)."""
@@ -87,8 +91,51 @@ def all_gather_shares(packed):
     return np.stack([p.cpu().numpy().reshape(-1) for p in parts])
 
 
+def _widenable(leaves) -> bool:
+    return all((kind == "int" and bits <= 64) or (kind == "intmodn" and 0 < mod <= (1 << 32))
+               for kind, bits, mod in leaves)
+
+
+def all_reduce_shares(leaves, packed, count: int):
+    """Group sum over ranks via one all_reduce(SUM) of the int64-widened leaves
+    (requires _widenable(leaves)); returns the packed host array."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    host = packed.cpu().numpy().reshape(count, -1) if hasattr(packed, "cpu") else \
+        np.asarray(packed, np.uint8).reshape(count, -1)
+    cols, off = [], 0
+    for kind, bits, mod in leaves:
+        w = bits // 8
+        raw = np.ascontiguousarray(host[:, off:off + w]).view(f"<u{w}").reshape(count)
+        cols.append(raw.astype(np.uint64).view(np.int64))
+        off += w
+    wide = torch.from_numpy(np.stack(cols, axis=1))
+    dev = packed.device if (hasattr(packed, "is_cuda") and packed.is_cuda
+                            and dist.get_backend() != "gloo") else torch.device("cpu")
+    wide = wide.to(dev)
+    dist.all_reduce(wide, op=dist.ReduceOp.SUM)
+    total = wide.cpu().numpy().view(np.uint64)
+    out = np.empty_like(host)
+    off = 0
+    for i, (kind, bits, mod) in enumerate(leaves):
+        w = bits // 8
+        v = total[:, i]
+        v = v % np.uint64(mod) if kind == "intmodn" else (
+            v & np.uint64((1 << bits) - 1) if bits < 64 else v)
+        out[:, off:off + w] = v.astype(f"<u{w}").view(np.uint8).reshape(count, w)
+        off += w
+    return out.reshape(-1)
+
+
 def aggregate_shares(dpf, hierarchy_level: int, packed, count: int):
     """Group sum over ranks of `count`-element packed partial sums: the
     cross-GPU step of the aggregation variant."""
+    import torch.distributed as dist
+    from . import dpf as D
+    leaves = D.leaves_of(dpf.parameters()[hierarchy_level].value_type)
+    if (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            and _widenable(leaves)):
+        return all_reduce_shares(leaves, packed, count)
     stacked = all_gather_shares(packed)
     return dpf.sum_packed_shares(hierarchy_level, stacked, stacked.shape[0], count)

@@ -100,7 +100,13 @@ def test_partition_helpers():
 
 
 # ------------------------------------------------- key-batch sharding (config 4/5)
-def _key_worker(rank, world, port, q):
+VTS = {"intmodn32x2": (("tuple", [("intmodn", 32, 4294967291)] * 2), [[1, 1]]),
+       "u64": (("int", 64), [[3]]),
+       "u16": (("int", 16), [[40000]]),
+       "u128": (("int", 128), [[5]])}   # u128: the all-gather fallback
+
+
+def _key_worker(rank, world, port, q, vt_name="intmodn32x2"):
     import torch
     import torch.distributed as dist
     from distributed_point_functions_amd import dpf as D
@@ -108,7 +114,7 @@ def _key_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        vt = ("tuple", [("intmodn", 32, 4294967291)] * 2)
+        vt, beta = VTS[vt_name]
         levels = [(16, vt, 64.0)]
         P = O.OracleParams(levels)
         dpf = D.DistributedPointFunction.create_incremental(params(levels))
@@ -116,7 +122,7 @@ def _key_worker(rank, world, port, q):
         n_keys, pts = 23, [0, 5, 77, 4095, 65535, 1234]
         rng = np.random.default_rng(17)          # same keys on every rank
         alphas = [int(a) for a in rng.integers(0, 1 << 16, size=n_keys)]
-        keys = [O.generate_keys(P, a, [[1, 1]], 1000 + k, 2000 + k)[k % 2]
+        keys = [O.generate_keys(P, a, beta, 1000 + k, 2000 + k)[k % 2]
                 for k, a in enumerate(alphas)]
         lo, hi = S.key_range(n_keys, world, rank)
         part = None
@@ -133,26 +139,30 @@ def _key_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_key_batch_shards_aggregate_to_full_sum(world):
+@pytest.mark.parametrize("world,vt_name", [(2, "intmodn32x2"), (3, "intmodn32x2"), (2, "u64"),
+                                           (3, "u16"), (2, "u128")])
+def test_key_batch_shards_aggregate_to_full_sum(world, vt_name):
+    """all_reduce(SUM) of widened leaves (ints <= 64 bits, IntModN32) or the
+    all-gather fallback (uint128) gives the sum over all keys."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_key_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_key_worker, args=(r, world, port, q, vt_name))
+             for r in range(world)]
     for p in procs:
         p.start()
     total = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    vt = ("tuple", [("intmodn", 32, 4294967291)] * 2)
+    vt, beta = VTS[vt_name]
     P = O.OracleParams([(16, vt, 64.0)])
     rng = np.random.default_rng(17)
     alphas = [int(a) for a in rng.integers(0, 1 << 16, size=23)]
     pts = [0, 5, 77, 4095, 65535, 1234]
     want = None
     for k, a in enumerate(alphas):
-        v = O.evaluate_at(P, O.generate_keys(P, a, [[1, 1]], 1000 + k, 2000 + k)[k % 2], 0, pts)
+        v = O.evaluate_at(P, O.generate_keys(P, a, beta, 1000 + k, 2000 + k)[k % 2], 0, pts)
         want = v if want is None else O.add_packed(vt, want, v)
     np.testing.assert_array_equal(total.reshape(want.shape), want)
 
