@@ -397,14 +397,29 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
     if (d < E) {
       const uint4 cs = cw_block(cws + d);
       const uint32_t cc = (uint32_t)(cl[d] & 1) | ((uint32_t)(cr[d] & 1) << 1);
-#pragma unroll
-      for (int i = (1 << d) - 1; i >= 0; --i) {
+      if (d == 0) {
         Block4 c0, c1;
         uint32_t t0, t1;
-        children_step(lk, p.rkl.k, p.rkr.k, N[i], (T >> i) & 1u, cs, cc, c0, t0, c1, t1);
-        N[2 * i] = c0;
-        N[2 * i + 1] = c1;
-        T = (T & ~(3u << (2 * i))) | (t0 << (2 * i)) | (t1 << (2 * i + 1));
+        children_step(lk, p.rkl.k, p.rkr.k, N[0], T & 1u, cs, cc, c0, t0, c1, t1);
+        N[0] = c0;
+        N[1] = c1;
+        T = t0 | (t1 << 1);
+      } else {
+        // Nodes i and i - 1 together (ILP4); descending i never overwrites an
+        // unread node.
+#pragma unroll
+        for (int i = (1 << d) - 1; i >= 1; i -= 2) {
+          Block4 c[4];
+          uint32_t t[4];
+          children_step_x2(lk, p.rkl.k, p.rkr.k, N[i], (T >> i) & 1u, N[i - 1], (T >> (i - 1)) & 1u,
+                           cs, cc, c, t);
+          N[2 * i] = c[0];
+          N[2 * i + 1] = c[1];
+          N[2 * i - 2] = c[2];
+          N[2 * i - 1] = c[3];
+          T = (T & ~(15u << (2 * i - 2))) | (t[2] << (2 * i - 2)) | (t[3] << (2 * i - 1)) |
+              (t[0] << (2 * i)) | (t[1] << (2 * i + 1));
+        }
       }
     }
   }

@@ -177,6 +177,26 @@ __device__ __forceinline__ void children_step(const LdsLookup& lk, const uint32_
   c1 = h1;
 }
 
+// children_step for two nodes of the same level (same correction word): the
+// four child hashes interleaved (ILP4).
+__device__ __forceinline__ void children_step_x2(const LdsLookup& lk, const uint32_t* rkl,
+                                                 const uint32_t* rkr, Block4 sa, uint32_t ta,
+                                                 Block4 sb, uint32_t tb, uint4 cs, uint32_t cctl,
+                                                 Block4* c, uint32_t* t) {
+  Block4 h[4] = {sa, sa, sb, sb};
+  const UniformRK rk[4] = {UniformRK{rkl}, UniformRK{rkr}, UniformRK{rkl}, UniformRK{rkr}};
+  dpf_aes::mmo_hashN<4>(h, lk, rk);
+  const uint32_t pt[4] = {ta, ta, tb, tb};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t m = 0u - pt[i];
+    h[i].w0 ^= cs.x & m; h[i].w1 ^= cs.y & m; h[i].w2 ^= cs.z & m; h[i].w3 ^= cs.w & m;
+    t[i] = (h[i].w0 & 1u) ^ (pt[i] & ((cctl >> (i & 1)) & 1u));
+    h[i].w0 &= ~1u;
+    c[i] = h[i];
+  }
+}
+
 // Path step with a per-lane direction bit (evaluate_prg_hwy.cc:452-486).
 __device__ __forceinline__ void path_step(const LdsLookup& lk, const RoundKeys& rkl,
                                           const RoundKeys& rkd, Block4& s, uint32_t& t,
