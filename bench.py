@@ -435,7 +435,25 @@ def main_evaluate_at(args):
     b0, b1 = dpf.generate_key_batch(alphas[lo:hi], [beta], root_seeds=seeds[2 * lo:2 * hi],
                                     threads=threads)
     keygen_s = time.perf_counter() - t0
-    dbatch = dpf.upload_key_batch(b0, stream=stream)
+    # Key ingestion: the rank's keys as serialized DpfKeys
+    # (the reference's wire format), parsed into the SoA batch on host threads
+    # and uploaded -- the path a server receiving client keys takes.
+    t0 = time.perf_counter()
+    wire = dpf.serialize_key_batch(b0, threads=threads)
+    serialize_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    parsed = dpf.parse_key_batch(wire, threads=threads)
+    parse_s = time.perf_counter() - t0
+    if not np.array_equal(parsed.seeds(), b0.seeds()):
+        raise SystemExit("parsed key batch differs from the generated one")
+    ingest = {"keys": nk, "wire_bytes": sum(len(w) for w in wire), "threads": threads,
+              "serialize_s": serialize_s, "parse_s": parse_s, "parse_keys_per_s": nk / parse_s}
+    del wire
+    t0 = time.perf_counter()
+    dbatch = dpf.upload_key_batch(parsed, stream=stream)
+    torch.cuda.synchronize(dev)
+    ingest["upload_s"] = time.perf_counter() - t0
+    del parsed
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
     if summed:
@@ -518,7 +536,7 @@ def main_evaluate_at(args):
                        "keys": n_keys, "points_per_key": ppk, "log_domain_size": 128,
                        "parallelism": f"key-batch x{world}"},
             "aes_blocks_per_s": n_keys * ppk * (depth + 1) * args.steps / elapsed,
-            "keygen_s_rank0": keygen_s, "keygen_threads": threads,
+            "keygen_s_rank0": keygen_s, "keygen_threads": threads, "key_ingest_rank0": ingest,
             "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
                          "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
                          "traffic": None,

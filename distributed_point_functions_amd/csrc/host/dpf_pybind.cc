@@ -229,6 +229,17 @@ class PyDpf {
     return PyKeyBatch{std::make_shared<KeyBatch>(Take(dpf_->MakeKeyBatch(MakeConstSpan(ptrs))))};
   }
   py::bytes KeyFromBatch(const PyKeyBatch& b, int64_t k) { return Ser(Take(dpf_->KeyFromBatch(*b.b, k))); }
+  py::list SerializeKeyBatch(const PyKeyBatch& b, int threads) {
+    StatusOr<std::vector<std::string>> r = InternalError("unset");
+    {
+      py::gil_scoped_release nogil;
+      r = dpf_->SerializeKeyBatch(*b.b, threads);
+    }
+    std::vector<std::string> v = Take(std::move(r));
+    py::list out(v.size());
+    for (size_t i = 0; i < v.size(); ++i) out[i] = py::bytes(v[i]);
+    return out;
+  }
   PyKeyBatch ParseKeyBatch(const std::vector<py::bytes>& keys, int threads) {
     std::vector<std::string_view> views;
     views.reserve(keys.size());
@@ -429,6 +440,7 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("make_key_batch", &PyDpf::MakeKeyBatch)
       .def("key_from_batch", &PyDpf::KeyFromBatch)
       .def("parse_key_batch", &PyDpf::ParseKeyBatch)
+      .def("serialize_key_batch", &PyDpf::SerializeKeyBatch)
       .def("generate_key_batch", &PyDpf::GenerateKeyBatch)
       .def("evaluate_at_batch_to_device", &PyDpf::EvaluateAtBatchToDevice)
       .def("evaluate_at_batch_sum_to_device", &PyDpf::EvaluateAtBatchSumToDevice)

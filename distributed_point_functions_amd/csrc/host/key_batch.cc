@@ -165,6 +165,17 @@ StatusOr<KeyBatch> DistributedPointFunction::ParseKeyBatch(Span<const std::strin
   return b;
 }
 
+StatusOr<std::vector<std::string>> DistributedPointFunction::SerializeKeyBatch(
+    const KeyBatch& b, int num_threads) const {
+  std::vector<std::string> out(b.num_keys);
+  DPF_RETURN_IF_ERROR(ParallelRows(b.num_keys, num_threads, [&](int64_t k) -> Status {
+    DPF_ASSIGN_OR_RETURN(DpfKey key, KeyFromBatch(b, k));
+    out[k] = key.SerializeAsString();
+    return OkStatus();
+  }));
+  return out;
+}
+
 StatusOr<DpfKey> DistributedPointFunction::KeyFromBatch(const KeyBatch& b, int64_t k) const {
   if (k < 0 || k >= b.num_keys) return InvalidArgumentError("key index out of range");
   const int H = static_cast<int>(parameters().size());

@@ -345,6 +345,11 @@ class DistributedPointFunction:
         on host threads (batched key ingestion)."""
         return _call(self._impl.parse_key_batch, list(serialized_keys), int(threads))
 
+    def serialize_key_batch(self, batch, threads: int = 0) -> List[bytes]:
+        """Every row of a key batch as a serialized DpfKey (inverse of
+        parse_key_batch), on host threads."""
+        return _call(self._impl.serialize_key_batch, batch, int(threads))
+
     def key_from_batch(self, batch, k: int) -> pb.DpfKey:
         key = pb.DpfKey()
         key.ParseFromString(_call(self._impl.key_from_batch, batch, int(k)))

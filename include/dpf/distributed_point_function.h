@@ -246,6 +246,10 @@ class DistributedPointFunction {
                                    int num_threads = 0) const;
   // Row k of `batch` as a DpfKey proto (inverse of MakeKeyBatch).
   StatusOr<DpfKey> KeyFromBatch(const KeyBatch& batch, int64_t k) const;
+  // Every row as a serialized DpfKey (inverse of ParseKeyBatch), on
+  // `num_threads` host threads (0 = hardware concurrency, at most 16).
+  StatusOr<std::vector<std::string>> SerializeKeyBatch(const KeyBatch& batch,
+                                                       int num_threads = 0) const;
   // Key generation for many alphas at once, straight into SoA form, on
   // `num_threads` host threads (0 = hardware concurrency).  Key k of the pair
   // is what GenerateKeysIncrementalWithSeeds(alphas[k], beta, root_seeds[2k],

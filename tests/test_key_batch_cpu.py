@@ -175,3 +175,22 @@ def test_parse_key_batch_matches_make_key_batch():
     bad[1700] = b"\xff\xff\xff"
     with pytest.raises(D.DpfStatusError, match="Failed to parse DpfKey 1700"):
         dpf.parse_key_batch(bad, threads=4)
+
+
+def test_serialize_key_batch_roundtrip():
+    # SerializeKeyBatch (threaded egress) is byte-identical to serializing each
+    # KeyFromBatch proto, and ParseKeyBatch of it restores the batch.
+    levels = [(10, ("int", 16), 0), (40, ("tuple", [("int", 32), ("intmodn", 64, G.M64)]), 48.0)]
+    dpf = make(levels)
+    rng = np.random.default_rng(5)
+    alphas = [int(a) for a in rng.integers(0, 1 << 40, size=2000)]
+    b0, b1 = dpf.generate_key_batch(alphas, betas_for(levels), root_seeds=seeds_array(rng, 2000),
+                                    threads=4)
+    for b in (b0, b1):
+        ser = dpf.serialize_key_batch(b, threads=4)
+        assert len(ser) == 2000
+        for k in (0, 999, 1999):
+            assert ser[k] == dpf.key_from_batch(b, k).SerializeToString()
+        back = dpf.parse_key_batch(ser, threads=4)
+        assert np.array_equal(back.seeds(), b.seeds())
+        assert dpf.serialize_key_batch(back, threads=1) == ser
