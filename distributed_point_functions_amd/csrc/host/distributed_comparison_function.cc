@@ -236,6 +236,7 @@ StatusOr<std::vector<uint8_t>> DistributedComparisonFunction::EvaluatePacked(
                              up.Ptr<dpf_block>(o_pts), up.Ptr<dpf_block>(o_cws),
                              up.Ptr<uint8_t>(o_cwl), up.Ptr<uint8_t>(o_cwr), L, vcw,
                              s->out.get(), nullptr));
+  DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
   std::vector<uint8_t> out(m * f.packed_size);
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
   return out;

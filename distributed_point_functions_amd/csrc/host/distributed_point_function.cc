@@ -580,6 +580,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
                                      up.Ptr<uint8_t>(o_cw.left), up.Ptr<uint8_t>(o_cw.right), &kl, &kr,
                                      &kv, &desc, cepb, up.Ptr<dpf_block>(o_vcw),
                                      ctx.key().party() & 1, expand_out, stream));
+  DPF_RETURN_IF_ERROR(up.MarkUsed(stream));
   void* result = expand_out;
   if (!identity) {
     std::vector<int64_t> offsets(num_prefixes);
@@ -772,6 +773,7 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
       up.Ptr<int32_t>(o_bi), up.Ptr<dpf_block>(o_cw.seed), up.Ptr<uint8_t>(o_cw.left),
       up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), s->out.get(),
       nullptr));
+  DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
   std::vector<uint8_t> out =
       dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(n) * f.packed_size);
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));

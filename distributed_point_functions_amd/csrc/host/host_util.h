@@ -217,10 +217,9 @@ class HostStaging {
   HostStaging(const HostStaging&) = delete;
   HostStaging& operator=(const HostStaging&) = delete;
   ~HostStaging() {
-    if (p_) {
-      (void)Drain();
-      dpf_hip_host_free(p_);
-    }
+    (void)Drain();
+    for (void* e : free_events_) dpf_hip_event_destroy(e);
+    if (p_) dpf_hip_host_free(p_);
   }
   Status Upload(DeviceBuffer& dst, const void* data, size_t bytes, void* stream) {
     DPF_RETURN_IF_ERROR(dst.Reserve(bytes));
@@ -242,20 +241,34 @@ class HostStaging {
     std::memcpy(src, data, bytes);
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(dst.get(), src, bytes, stream));
     used_ += (bytes + 255) & ~size_t{255};
-    if (std::find(streams_.begin(), streams_.end(), stream) == streams_.end())
-      streams_.push_back(stream);
-    return OkStatus();
+    // One event per stream since the last wrap, re-recorded after each copy.
+    for (auto& [st, ev] : pending_)
+      if (st == stream) return FromHip(dpf_hip_event_record(ev, stream));
+    void* ev = nullptr;
+    if (!free_events_.empty()) {
+      ev = free_events_.back();
+      free_events_.pop_back();
+    } else {
+      HIP_RETURN_IF_ERROR(dpf_hip_event_create(&ev));
+    }
+    pending_.emplace_back(stream, ev);
+    return FromHip(dpf_hip_event_record(ev, stream));
   }
 
  private:
   Status Drain() {
-    for (void* st : streams_) HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(st));
-    streams_.clear();
+    for (auto& [st, ev] : pending_) {
+      HIP_RETURN_IF_ERROR(dpf_hip_event_sync(ev));
+      free_events_.push_back(ev);
+    }
+    pending_.clear();
     return OkStatus();
   }
   void* p_ = nullptr;
   size_t cap_ = 0, used_ = 0;
-  std::vector<void*> streams_;   // streams with copies from the ring since it last wrapped
+  // (stream, event after its last copy) for copies from the ring since it wrapped.
+  std::vector<std::pair<void*, void*>> pending_;
+  std::vector<void*> free_events_;
 };
 
 // The small argument arrays of ONE call packed into one image and copied with
@@ -270,15 +283,23 @@ class PackedUploads {
   PackedUploads(const PackedUploads&) = delete;
   PackedUploads& operator=(const PackedUploads&) = delete;
   ~PackedUploads() {
-    if (pinned_) {
-      if (pending_) (void)dpf_hip_stream_sync(stream_);
-      dpf_hip_host_free(pinned_);
-    }
+    if (pending_) (void)dpf_hip_event_sync(event_);
+    if (event_) dpf_hip_event_destroy(event_);
+    if (pinned_) dpf_hip_host_free(pinned_);
   }
+  // Waits for the previous call's copy and kernel (an event recorded on its
+  // stream after the launch, MarkUsed) before the buffers are rewritten.
   Status Reset() {
-    if (pending_) HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream_));
+    if (pending_) HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
     pending_ = false;
     image_.clear();
+    return OkStatus();
+  }
+  // Records that the work queued on `stream` so far reads the arena.
+  Status MarkUsed(void* stream) {
+    if (!event_) HIP_RETURN_IF_ERROR(dpf_hip_event_create(&event_));
+    HIP_RETURN_IF_ERROR(dpf_hip_event_record(event_, stream));
+    pending_ = true;
     return OkStatus();
   }
   template <typename T>
@@ -306,9 +327,7 @@ class PackedUploads {
     DPF_RETURN_IF_ERROR(arena_.Reserve(cap_));
     std::memcpy(pinned_, image_.data(), bytes);
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(arena_.get(), pinned_, bytes, stream));
-    pending_ = true;
-    stream_ = stream;
-    return OkStatus();
+    return MarkUsed(stream);
   }
   template <typename T>
   T* Ptr(size_t off) const {
@@ -322,7 +341,7 @@ class PackedUploads {
   size_t cap_ = 0;
   DeviceBuffer arena_;
   bool pending_ = false;
-  void* stream_ = nullptr;
+  void* event_ = nullptr;
 };
 
 class DeviceScratch {

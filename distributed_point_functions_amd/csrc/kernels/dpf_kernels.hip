@@ -722,6 +722,10 @@ int dpf_hip_stream_sync(void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   return kOk;
 }
+int dpf_hip_event_sync(void* event) {
+  HIP_TRY(hipEventSynchronize((hipEvent_t)event));
+  return kOk;
+}
 int dpf_hip_packed_element_size(const dpf_value_desc* desc) {
   if (!desc) return -1;
   return packed_size(desc);

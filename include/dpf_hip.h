@@ -93,6 +93,11 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memset(void* dst, int value, size_t bytes, void* stream);
 int dpf_hip_stream_sync(void* stream);
+/* Waits for an event (dpf_hip_event_create/record, declared with the timing
+ * helpers below).  The host API marks the end of the work that reads its
+ * staging buffers with one, so reusing them never depends on the caller's
+ * stream still existing. */
+int dpf_hip_event_sync(void* event);
 /* Packed size in bytes of one output element: sum of leaf bits / 8. */
 int dpf_hip_packed_element_size(const dpf_value_desc* desc);
 
