@@ -92,7 +92,9 @@ struct Block4 {
 DPF_HD Block4 sigma(Block4 x) { return Block4{x.w2, x.w3, x.w2 ^ x.w0, x.w3 ^ x.w1}; }
 
 // Generic AES-128 encryption.  `LK` provides lookup<T, K>(w) = T_T[byte K of w]
-// and xor3(a, b, c).  `RK` provides rk(i) for round-key word i (0..43).
+// and xor3(a, b, c).  `RK` provides rk(i) for round-key word i (0..43) and
+// rk.mix(lk, a, b, i) = a ^ b ^ rk(i) (the round's last XOR, where a key
+// choice can be folded in: SelectRK in dpf_device.h).
 template <class LK, class RK>
 DPF_HD Block4 encrypt(Block4 s, const LK& lk, const RK& rk) {
   uint32_t w0 = s.w0 ^ rk(0), w1 = s.w1 ^ rk(1), w2 = s.w2 ^ rk(2), w3 = s.w3 ^ rk(3);
@@ -108,10 +110,10 @@ DPF_HD Block4 encrypt(Block4 s, const LK& lk, const RK& rk) {
                           lk.template lookup<2, 2>(w0));
     uint32_t n3 = lk.xor3(lk.template lookup<0, 0>(w3), lk.template lookup<1, 1>(w0),
                           lk.template lookup<2, 2>(w1));
-    n0 = lk.xor3(n0, lk.template lookup<3, 3>(w3), rk(4 * r + 0));
-    n1 = lk.xor3(n1, lk.template lookup<3, 3>(w0), rk(4 * r + 1));
-    n2 = lk.xor3(n2, lk.template lookup<3, 3>(w1), rk(4 * r + 2));
-    n3 = lk.xor3(n3, lk.template lookup<3, 3>(w2), rk(4 * r + 3));
+    n0 = rk.mix(lk, n0, lk.template lookup<3, 3>(w3), 4 * r + 0);
+    n1 = rk.mix(lk, n1, lk.template lookup<3, 3>(w0), 4 * r + 1);
+    n2 = rk.mix(lk, n2, lk.template lookup<3, 3>(w1), 4 * r + 2);
+    n3 = rk.mix(lk, n3, lk.template lookup<3, 3>(w2), 4 * r + 3);
     w0 = n0; w1 = n1; w2 = n2; w3 = n3;
   }
   // Last round: S-box bytes pulled out of T2/T3/T0/T1 for rows 0/1/2/3.
@@ -165,14 +167,14 @@ DPF_HD void encrypt2(Block4& sa, Block4& sb, const LK& lk, const RKA& ra, const 
                           lk.template lookup<2, 2>(b0));
     uint32_t m3 = lk.xor3(lk.template lookup<0, 0>(b3), lk.template lookup<1, 1>(b0),
                           lk.template lookup<2, 2>(b1));
-    n0 = lk.xor3(n0, lk.template lookup<3, 3>(a3), ra(4 * r + 0));
-    n1 = lk.xor3(n1, lk.template lookup<3, 3>(a0), ra(4 * r + 1));
-    n2 = lk.xor3(n2, lk.template lookup<3, 3>(a1), ra(4 * r + 2));
-    n3 = lk.xor3(n3, lk.template lookup<3, 3>(a2), ra(4 * r + 3));
-    m0 = lk.xor3(m0, lk.template lookup<3, 3>(b3), rb(4 * r + 0));
-    m1 = lk.xor3(m1, lk.template lookup<3, 3>(b0), rb(4 * r + 1));
-    m2 = lk.xor3(m2, lk.template lookup<3, 3>(b1), rb(4 * r + 2));
-    m3 = lk.xor3(m3, lk.template lookup<3, 3>(b2), rb(4 * r + 3));
+    n0 = ra.mix(lk, n0, lk.template lookup<3, 3>(a3), 4 * r + 0);
+    n1 = ra.mix(lk, n1, lk.template lookup<3, 3>(a0), 4 * r + 1);
+    n2 = ra.mix(lk, n2, lk.template lookup<3, 3>(a1), 4 * r + 2);
+    n3 = ra.mix(lk, n3, lk.template lookup<3, 3>(a2), 4 * r + 3);
+    m0 = rb.mix(lk, m0, lk.template lookup<3, 3>(b3), 4 * r + 0);
+    m1 = rb.mix(lk, m1, lk.template lookup<3, 3>(b0), 4 * r + 1);
+    m2 = rb.mix(lk, m2, lk.template lookup<3, 3>(b1), 4 * r + 2);
+    m3 = rb.mix(lk, m3, lk.template lookup<3, 3>(b2), 4 * r + 3);
     a0 = n0; a1 = n1; a2 = n2; a3 = n3;
     b0 = m0; b1 = m1; b2 = m2; b3 = m3;
   }
@@ -227,7 +229,7 @@ DPF_UNROLL
     for (int i = 0; i < N; ++i) {
 DPF_UNROLL
       for (int c = 0; c < 4; ++c)
-        n[i][c] = lk.xor3(n[i][c], lk.template lookup<3, 3>(w[i][(c + 3) & 3]), rk[i](4 * r + c));
+        n[i][c] = rk[i].mix(lk, n[i][c], lk.template lookup<3, 3>(w[i][(c + 3) & 3]), 4 * r + c);
     }
 DPF_UNROLL
     for (int i = 0; i < N; ++i)
@@ -276,6 +278,8 @@ struct HostLookup {
 struct ArrayRK {
   const uint32_t* k;
   DPF_HD uint32_t operator()(int i) const { return k[i]; }
+  template <class LK>
+  DPF_HD uint32_t mix(const LK& lk, uint32_t a, uint32_t b, int i) const { return lk.xor3(a, b, k[i]); }
 };
 
 }  // namespace dpf_aes

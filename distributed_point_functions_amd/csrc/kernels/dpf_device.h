@@ -118,13 +118,25 @@ __device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds) {
 struct UniformRK {
   const uint32_t* k;
   __device__ __forceinline__ uint32_t operator()(int i) const { return k[i]; }
+  template <class LK>
+  __device__ __forceinline__ uint32_t mix(const LK& lk, uint32_t a, uint32_t b, int i) const {
+    return lk.xor3(a, b, k[i]);
+  }
 };
-// Per-lane key choice: rk = left ^ (mask & (left ^ right)).
+// Per-lane key choice: rk = left ^ (mask & (left ^ right)).  In a round's last
+// XOR the choice costs one bitop3: (a ^ b ^ left) ^ (mask & diff), each
+// instruction reading one scalar key word (a VALU op reads at most one SGPR;
+// the plain form needed a v_mov of the key word first).
 struct SelectRK {
   const uint32_t* left;
   const uint32_t* diff;
   uint32_t mask;
   __device__ __forceinline__ uint32_t operator()(int i) const { return left[i] ^ (mask & diff[i]); }
+  template <class LK>
+  __device__ __forceinline__ uint32_t mix(const LK& lk, uint32_t a, uint32_t b, int i) const {
+    // bitop3 truth table index = S0*4 + S1*2 + S2; 0x78 = S0 ^ (S1 & S2).
+    return __builtin_amdgcn_bitop3_b32(lk.xor3(a, b, left[i]), mask, diff[i], 0x78);
+  }
 };
 
 using dpf_aes::Block4;

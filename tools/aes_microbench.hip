@@ -51,7 +51,12 @@ struct L1 {  // 1 table x 32 copies = 32 KiB, rotations in VALU
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
 };
-struct URK { const uint32_t* k; __device__ __forceinline__ uint32_t operator()(int i) const { return k[i]; } };
+struct URK {
+  const uint32_t* k;
+  __device__ __forceinline__ uint32_t operator()(int i) const { return k[i]; }
+  template <class LK>
+  __device__ __forceinline__ uint32_t mix(const LK& lk, uint32_t a, uint32_t b, int i) const { return lk.xor3(a, b, k[i]); }
+};
 // 4 tables in 256-byte rows: row e = [A copies 0..31 | B copies 0..31], C|D at +64 KiB.
 // Address = v_perm_b32(w, lane_reg[T], sel_K): byte0 = lane offset (+128 for B/D),
 // byte1 = byte K of w (the entry), byte2 = 1 for C/D.
