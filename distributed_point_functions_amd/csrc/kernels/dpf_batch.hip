@@ -441,7 +441,7 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
 }
 
 template <class V, int MAXE, bool SUM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void batch_level_kernel(
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
     BatchLevelParams p, V v) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
@@ -841,7 +841,7 @@ struct DcfParams {
 __device__ __forceinline__ u128 shr128(u128 x, int s) { return s >= 128 ? (u128)0 : x >> s; }
 
 template <int BITS, bool FAST>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void dcf_eval_kernel(
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
     DcfParams p, DcfLevels lv, GenericLeaf g) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);

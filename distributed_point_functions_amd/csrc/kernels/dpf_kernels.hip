@@ -54,7 +54,7 @@ namespace {
 // Kernels
 // ------------------------------------------------------------------------
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void hash_kernel(int64_t n, const dpf_block* __restrict__ in,
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void hash_kernel(int64_t n, const dpf_block* __restrict__ in,
                                                       dpf_block* __restrict__ out,
                                                       RoundKeys rk) {
   __shared__ LdsImage lds;
@@ -82,7 +82,7 @@ struct PathParams {
 };
 
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void eval_paths_kernel(PathParams p) {
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_paths_kernel(PathParams p) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
@@ -117,7 +117,7 @@ struct ExpandParams {
 };
 
 template <class Leaf>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void expand_kernel(ExpandParams p, Leaf leaf) {
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   leaf.init();
   fill_tables(lds.tab);
@@ -250,7 +250,7 @@ struct PointParams {
 };
 
 template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) void eval_points_kernel(PointParams p, Leaf leaf) {
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(PointParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
@@ -432,7 +432,7 @@ int block_for(int64_t work_items) {
 
 int grid_for(int64_t work_items, int block) {
   int64_t g = (work_items + block - 1) / block;
-  int64_t cap = num_cus();  // one 128 KiB-LDS workgroup per CU
+  int64_t cap = num_cus() * kWgPerCu;  // one 128 KiB-LDS workgroup per CU
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
@@ -801,11 +801,14 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
   if (num_starts > (INT64_MAX >> num_levels))
     return fail(kInvalidArgument, "expansion too large");
   // Choose the depth-first subtree depth S and the per-item walk depth k0.
-  const int64_t threads = (int64_t)num_cus() * kBlock;
+  const int64_t threads = (int64_t)num_cus() * kWgPerCu * kBlock;
   int S = num_levels < kSMax ? num_levels : kSMax;
   // Small trees: shallow subtrees and more items, so that a launch far below
   // one full workgroup per CU is not serialised on a few lanes' DFS.
   while (S > 1 && (num_starts << (num_levels - S)) < threads) --S;
+#if defined(DPF_FORCE_S)
+  if (num_levels >= DPF_FORCE_S) S = DPF_FORCE_S;  // variant builds (tools/variant_bench.py)
+#endif
   ExpandParams p;
   p.num_levels = num_levels;
   p.S = S;

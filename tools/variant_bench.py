@@ -62,6 +62,18 @@ def run_one():
     res["expand_ms"] = ms
     res["expand_gaes"] = (2 * (2**D - 1) + 2**D) / ms / 1e6
     del out
+    # expand from 5 start seeds x 27 levels (5 * 2^28 uint64 outputs): with
+    # S = 9 the 5 * 2^18 items divide evenly over 1024- and 640-thread
+    # workgroups alike (variants built with -DDPF_FORCE_S=9)
+    D5 = 27
+    seeds5 = rand_blocks(5)
+    ctrl5 = torch.tensor([0, 1, 0, 1, 1], dtype=torch.uint8, device=dev)
+    out = torch.empty(5 * (1 << 28) * 8, dtype=torch.uint8, device=dev)
+    ms = timed(lambda: H.expand(seeds5, ctrl5, cws[:D5], cl[:D5], cr[:D5], keys, desc, 2, vcw, 0,
+                                out=out))
+    res["expand5_ms"] = ms
+    res["expand5_gaes"] = 5 * (2 * (2**D5 - 1) + 2**D5) / ms / 1e6
+    del out
     # batched points, 2^16 keys x 2^10 points, log 128
     nk, ppk, Lv = 1 << 16, 1 << 10, 127
     kseed = rand_blocks(nk)
