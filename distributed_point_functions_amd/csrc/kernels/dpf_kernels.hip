@@ -249,7 +249,10 @@ struct PointParams {
   RoundKeys rkl, rkd, rkv;
 };
 
-template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM>
+// PAIRED = false (launches below one wave per CU, never in sum mode): one
+// chain per lane, half = P, so a small call spreads over twice the CUs and each
+// wave's dependent AES chain issues half the LDS reads per round.
+template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM, bool PAIRED = true>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(PointParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
@@ -305,14 +308,21 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(Poin
         const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
         const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
                                     (uint32_t)(c.high >> 32));
-        path_step2(lk, p.rkl, p.rkd, s0, t0, b0, s1, t1, b1, cs, cctl);
+        if constexpr (PAIRED)
+          path_step2(lk, p.rkl, p.rkd, s0, t0, b0, s1, t1, b1, cs, cctl);
+        else
+          path_step(lk, p.rkl, p.rkd, s0, t0, b0, cs, cctl);
       }
       const dpf_block* vcw = p.vcw + k * p.vcw_stride;
       if constexpr (FAST) {
         Block4 h0 = s0, h1 = s1;
-        dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+        if constexpr (PAIRED)
+          dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+        else
+          h0 = dpf_aes::mmo_hash(h0, lk, UniformRK{p.rkv.k});
         const u128 v0 = fast_point_value<BITS>(h0, t0, bi0, dpf_u128(vcw[bi0]), party, p.xor_mode);
-        const u128 v1 = fast_point_value<BITS>(h1, t1, bi1, dpf_u128(vcw[bi1]), party, p.xor_mode);
+        const u128 v1 =
+            PAIRED ? fast_point_value<BITS>(h1, t1, bi1, dpf_u128(vcw[bi1]), party, p.xor_mode) : v0;
         if (SUM) {
           acc0[0] = p.xor_mode ? (acc0[0] ^ v0) : (acc0[0] + v0);
           acc1[0] = p.xor_mode ? (acc1[0] ^ v1) : (acc1[0] + v1);
@@ -489,7 +499,26 @@ int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf
 }
 
 template <class Leaf, int BITS, bool FAST, bool SUM>
-int launch_points_t(const PointParams& p, const Leaf& leaf, hipStream_t s) {
+int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
+  if constexpr (!SUM) {
+    // Fewer paired items than one wave per CU: latency-bound, run unpaired.
+    if (pp.num_items < (int64_t)num_cus() * 64) {
+      PointParams p = pp;
+      p.half = p.points_per_key;
+      p.num_items = p.num_keys * p.points_per_key;
+      const int blk = block_for(p.num_items);
+      const dim3 grid(grid_for(p.num_items, blk)), block(blk);
+      if (p.half % 64 == 0)
+        hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, true, false, false>), grid, block,
+                           0, s, p, leaf);
+      else
+        hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, false, false, false>), grid,
+                           block, 0, s, p, leaf);
+      HIP_TRY(hipGetLastError());
+      return kOk;
+    }
+  }
+  const PointParams& p = pp;
   const int blk = block_for(p.num_items);
   const dim3 grid(grid_for(p.num_items, blk)), block(blk);
   if (p.half % 64 == 0)
