@@ -220,3 +220,11 @@ def test_eval_points_many_keys(hip, levels):
 
 def test_eval_points_from_partials(hip):
     _points_case(hip, np.random.default_rng(11), ("xor", 128), 5, 100, 12, from_partials=True)
+
+
+# Either side of the launcher's pairing threshold (paired items < one wave per
+# CU run unpaired; 256 CUs -> 16384 items = 32768 points of one key).
+@pytest.mark.parametrize("vt,ppk", [(("int", 64), 32765), (("int", 64), 32767),
+                                    (("xor", 128), 40001), (GENERIC_TYPES[0], 33001)], ids=str)
+def test_eval_points_pairing_threshold(hip, vt, ppk):
+    _points_case(hip, np.random.default_rng(ppk), vt, 1, ppk, 20)
