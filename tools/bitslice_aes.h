@@ -380,3 +380,77 @@ BS_HD void encrypt_loop1(uint32_t* s, const uint32_t* rk) {
 }
 
 }  // namespace bs
+
+namespace bs {
+
+// Lower-pressure round for 2 waves/SIMD: key masks from a VGPR key word
+// (v_bfe_i32 per plane, consumed at once) and the row moves as in-place
+// cycles with one temporary each.
+BS_HD uint32_t key_mask(uint32_t kw, int bit) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return (uint32_t)__builtin_amdgcn_sbfe((int)kw, bit, 1);
+#else
+  return 0u - ((kw >> bit) & 1u);
+#endif
+}
+
+template <int R>
+BS_HD void ark_phys_v(uint32_t* s, const uint32_t* rk4) {
+BS_UNROLL
+  for (int c = 0; c < 4; ++c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Keep the word in a VGPR so the masks are VALU ops, not 32 live SGPRs.
+    uint32_t kw = rk4[c];
+    asm volatile("v_mov_b32 %0, %1" : "=v"(kw) : "s"(kw));
+#else
+    const uint32_t kw = rk4[c];
+#endif
+BS_UNROLL
+    for (int r = 0; r < 4; ++r)
+BS_UNROLL
+      for (int i = 0; i < 8; ++i) s[8 * phys<R>(r, c) + i] ^= key_mask(kw, 8 * r + i);
+  }
+}
+
+BS_HD void restore_after1_cycles(uint32_t* s) {
+BS_UNROLL
+  for (int i = 0; i < 8; ++i) {
+    // Row 1: logical (1,c) sits at physical column c+1: rotate left by one.
+    uint32_t t = s[8 * (4 * 0 + 1) + i];
+    s[8 * (4 * 0 + 1) + i] = s[8 * (4 * 1 + 1) + i];
+    s[8 * (4 * 1 + 1) + i] = s[8 * (4 * 2 + 1) + i];
+    s[8 * (4 * 2 + 1) + i] = s[8 * (4 * 3 + 1) + i];
+    s[8 * (4 * 3 + 1) + i] = t;
+    // Row 2: two swaps.
+    t = s[8 * (4 * 0 + 2) + i];
+    s[8 * (4 * 0 + 2) + i] = s[8 * (4 * 2 + 2) + i];
+    s[8 * (4 * 2 + 2) + i] = t;
+    t = s[8 * (4 * 1 + 2) + i];
+    s[8 * (4 * 1 + 2) + i] = s[8 * (4 * 3 + 2) + i];
+    s[8 * (4 * 3 + 2) + i] = t;
+    // Row 3: logical (3,c) at physical column c+3: rotate right by one.
+    t = s[8 * (4 * 3 + 3) + i];
+    s[8 * (4 * 3 + 3) + i] = s[8 * (4 * 2 + 3) + i];
+    s[8 * (4 * 2 + 3) + i] = s[8 * (4 * 1 + 3) + i];
+    s[8 * (4 * 1 + 3) + i] = s[8 * (4 * 0 + 3) + i];
+    s[8 * (4 * 0 + 3) + i] = t;
+  }
+}
+
+BS_HD void encrypt_lowreg(uint32_t* s, const uint32_t* rk) {
+  add_round_key(s, rk);
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll 1
+#endif
+  for (int r = 1; r < 10; ++r) {
+    sub_bytes(s);
+    mix_inplace<1>(s);
+    ark_phys_v<1>(s, rk + 4 * r);
+    restore_after1_cycles(s);
+  }
+  sub_bytes(s);
+  ark_phys_v<1>(s, rk + 40);
+  restore_after1_cycles(s);
+}
+
+}  // namespace bs

@@ -52,7 +52,9 @@ __global__ __launch_bounds__(256) BS_WAVES_ATTR void bs_kernel(Keys kk, const ui
 #pragma unroll
     for (int i = 0; i < 44; ++i) k.rk[i] = rkg[i];
     if (MODE == 1 && it) bs::to_planes(blk, s);
-#if defined(BS_LOOP1)
+#if defined(BS_LOWREG)
+    bs::encrypt_lowreg(s, k.rk);
+#elif defined(BS_LOOP1)
     bs::encrypt_loop1(s, k.rk);
 #elif defined(BS_LOOP2)
     bs::encrypt_loop2(s, k.rk);
@@ -128,6 +130,10 @@ tdone:
       if (memcmp(back, back2, sizeof back)) ++bad;
       bs::to_planes(blk, s2);
       bs::encrypt_loop1(s2, rk);
+      bs::from_planes(s2, back2);
+      if (memcmp(back, back2, sizeof back)) ++bad;
+      bs::to_planes(blk, s2);
+      bs::encrypt_lowreg(s2, rk);
       bs::from_planes(s2, back2);
       if (memcmp(back, back2, sizeof back)) ++bad;
     }
