@@ -123,6 +123,12 @@ BS_HD void sub_bytes(uint32_t* s) {
 BS_UNROLL
   for (int j = 0; j < 16; ++j) {
     sbox(s + 8 * j);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BS_OPAQUE)
+    // Opaque S-box outputs: stop IR reassociation from merging the S-box's
+    // last XORs with MixColumns' XOR trees across all 16 bytes.
+BS_UNROLL
+    for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(s[8 * j + i]));
+#endif
     BS_FENCE_POINT();
   }
 }
