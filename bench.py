@@ -41,13 +41,14 @@ sys.path.insert(0, ROOT)
 
 LOG_PER_GPU = 30          # 2^30 uint64 outputs per GPU (BASELINE.json configs[1])
 # AES-128 rooflines (DESIGN.md "Roofline"), 256 CUs at 2.4 GHz:
-#  * LDS: a T-table block needs 160 conflict-free ds_read_b32 lookups = 640 B at
-#    128 B/clk/CU -> 5 clk/block/CU -> 122.9 G blocks/s.  This binds the
-#    T-table design the kernels use, so it is the `roofline` peak.
-#  * VALU: 320 lane-ops/block at 4 SIMD-32 x 32 lanes = 128 lane-ops/clk/CU ->
-#    2.5 clk/block/CU -> 245.8 G blocks/s (reported as `roofline_valu`).
-AES_PEAK_GBLOCKS = 122.9
+#  * VALU (the north_star's "integer-VALU AES roofline", the `roofline` object):
+#    C_AES = 320 lane-ops/block (10 rounds x (16 byte extractions + 16 XOR
+#    combines)) at 4 SIMD-32 x 32 lanes = 128 lane-ops/clk/CU -> 2.5 clk/block/CU
+#    -> 245.8 G blocks/s.
+#  * LDS (`roofline_lds`, the bound of the T-table design): 160 conflict-free
+#    ds_read_b32 lookups = 640 B at 128 B/clk/CU -> 5 clk/block/CU -> 122.9 G.
 AES_VALU_PEAK_GBLOCKS = 245.8
+AES_LDS_PEAK_GBLOCKS = 122.9
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
 METRIC = "DPF leaf evals/sec, full-domain 2^30 uint64 at 1/2/4/8 GPUs; AES blocks/s"
 KERNEL = "expand_kernel<FastIntLeaf<64, false> >"
@@ -214,6 +215,19 @@ def profiled_traffic(leaves_per_launch: int):
     return best
 
 
+def aes_rooflines(achieved: float, kernel: str, **extra) -> dict:
+    """`roofline` against the integer-VALU AES roofline (north_star, SURVEY.md
+    8d) and `roofline_lds` against the T-table's LDS bound, same achieved rate
+    (algorithmic AES blocks per launch / HIP-event launch time)."""
+    return {
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": AES_VALU_PEAK_GBLOCKS,
+                     "unit": "G AES-128 blocks/s", "frac": achieved / AES_VALU_PEAK_GBLOCKS,
+                     "kernel": kernel, **extra},
+        "roofline_lds": {"bound": "lds", "achieved": achieved, "peak": AES_LDS_PEAK_GBLOCKS,
+                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_LDS_PEAK_GBLOCKS},
+    }
+
+
 def init_ranks(torch, dist):
     """One process per GPU (RANK/LOCAL_RANK/WORLD_SIZE from torch.distributed.run),
     RCCL process group for N > 1.  Returns (world, rank, local, coll), `coll`
@@ -308,6 +322,7 @@ def main():
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
     kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
+    ginfo = S.group_info(kern_ms, device=coll)
 
     # Spot-check the last step's output (sum of the two parties' shares is beta
     # at alpha, 0 elsewhere) on a few positions of this rank's shard.
@@ -340,17 +355,13 @@ def main():
                        "outputs_per_gpu": outputs_per_rank, "tree_levels_per_gpu": depth,
                        "parallelism": f"subtree-prefix x{world}"},
             "aes_blocks_per_s": aes_per_launch * world * args.steps / elapsed,
-            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
-                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
-                         "traffic": tr[0] if tr else None,
-                         "traffic_source": tr[1] if tr else None,
-                         "pmc": tr[2] if tr else None,
-                         "kernel": KERNEL.replace("64", str(bits)), "launch_ms": kern_ms_max,
-                         "algorithmic_aes_per_launch": aes_per_launch,
-                         "algorithmic_bytes_per_launch": bytes_per_launch},
-            "roofline_valu": {"bound": "valu", "achieved": achieved,
-                              "peak": AES_VALU_PEAK_GBLOCKS, "unit": "G AES-128 blocks/s",
-                              "frac": achieved / AES_VALU_PEAK_GBLOCKS},
+            **aes_rooflines(achieved, KERNEL.replace("64", str(bits)),
+                            traffic=tr[0] if tr else None,
+                            traffic_source=tr[1] if tr else None,
+                            pmc=tr[2] if tr else None, launch_ms=kern_ms_max,
+                            algorithmic_aes_per_launch=aes_per_launch,
+                            algorithmic_bytes_per_launch=bytes_per_launch),
+            "process_group": ginfo,
             "roofline_hbm": {"bound": "hbm",
                              "achieved": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -497,6 +508,7 @@ def main_evaluate_at(args):
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
     kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
+    ginfo = S.group_info(kern_ms, device=coll)
 
     # Correctness spot checks outside the timed region.
     if summed:
@@ -537,12 +549,10 @@ def main_evaluate_at(args):
                        "parallelism": f"key-batch x{world}"},
             "aes_blocks_per_s": n_keys * ppk * (depth + 1) * args.steps / elapsed,
             "keygen_s_rank0": keygen_s, "keygen_threads": threads, "key_ingest_rank0": ingest,
-            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
-                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
-                         "traffic": None,
-                         "kernel": "eval_points_kernel<GenericLeaf, 64, true, true, %s>" %
-                                   ("true" if summed else "false"),
-                         "launch_ms": kern_ms_max, "algorithmic_aes_per_launch": aes_per_launch},
+            **aes_rooflines(achieved, "eval_points_kernel<GenericLeaf, 64, true, true, %s>" %
+                            ("true" if summed else "false"), traffic=None,
+                            launch_ms=kern_ms_max, algorithmic_aes_per_launch=aes_per_launch),
+            "process_group": ginfo,
         }
         if world == 1 and not args.no_cpu_baseline:
             host_pts = None if summed else points.view(-1, 2)
@@ -696,6 +706,7 @@ def main_heavy_hitters(args):
     kern_ms = sum(a.elapsed_ms(b) for a, b in evs) / args.steps
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
     kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
+    ginfo = S.group_info(kern_ms, device=coll)
     if rank == 0:
         HH.verify(record, logs, values, idx)        # every level, untimed
     outputs_per_pass = sum(len(v) for _, v, _, _ in record) * n_keys * 2
@@ -725,11 +736,9 @@ def main_heavy_hitters(args):
             "keygen_s_rank0": keygen_s, "keygen_threads": threads,
             "verified": "two-server reconstruction == plaintext prefix histogram at every level",
             "true_top_k_recall": len(true_top & set(final)) / max(len(true_top), 1),
-            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
-                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
-                         "traffic": None, "kernel": "batch_level_kernel<Mod32V, 2, true>",
-                         "launch_ms_per_pass": kern_ms_max,
-                         "algorithmic_aes_per_pass": aes_rank},
+            **aes_rooflines(achieved, "batch_level_kernel<Mod32V, 2, true>", traffic=None,
+                            launch_ms_per_pass=kern_ms_max, algorithmic_aes_per_pass=aes_rank),
+            "process_group": ginfo,
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_heavy_hitters(logs, record, alphas, seeds,
@@ -808,6 +817,7 @@ def main_dcf(args):
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
     kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
+    ginfo = S.group_info(kern_ms, device=coll)
     # Spot check against the single-key API (itself parity-tested vs the oracle).
     host_pts = pts.cpu().numpy().view(np.uint64)
     for k in (0, nk - 1):
@@ -833,10 +843,9 @@ def main_dcf(args):
                        "log_domain_size": n, "parallelism": f"key-batch x{world}"},
             "aes_blocks_per_s": n_keys * ppk * aes_per_eval * args.steps / elapsed,
             "keygen_s_rank0": keygen_s,
-            "roofline": {"bound": "lds", "achieved": achieved, "peak": AES_PEAK_GBLOCKS,
-                         "unit": "G AES-128 blocks/s", "frac": achieved / AES_PEAK_GBLOCKS,
-                         "traffic": None, "kernel": "dcf_eval_kernel<64, true>",
-                         "launch_ms": kern_ms_max, "algorithmic_aes_per_launch": aes_launch},
+            **aes_rooflines(achieved, "dcf_eval_kernel<64, true>", traffic=None,
+                            launch_ms=kern_ms_max, algorithmic_aes_per_launch=aes_launch),
+            "process_group": ginfo,
         }
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))

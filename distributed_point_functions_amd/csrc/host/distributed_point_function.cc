@@ -497,8 +497,22 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     return InvalidArgumentError(
         "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
 
-  // Unique tree indices of the prefixes, in first-seen order (h:718-742).
+  // The output size is known before anything touches `ctx`: a too-small
+  // device buffer is rejected here, so the caller can retry with the same
+  // context and a larger buffer.
   const int64_t num_prefixes = static_cast<int64_t>(prefixes.size());
+  {
+    const int64_t per_prefix = int64_t{1} << (log_domain_size - previous_log_domain_size);
+    const int64_t out_total =
+        num_prefixes == 0
+            ? (int64_t{1} << hierarchy_to_tree()[hierarchy_level]) *
+                  corrected_elements_per_block(hierarchy_level)
+            : num_prefixes * per_prefix;
+    if (device_out && capacity_bytes < out_total * flat_[hierarchy_level].packed_size)
+      return InvalidArgumentError("device output buffer too small");
+  }
+
+  // Unique tree indices of the prefixes, in first-seen order (h:718-742).
   std::vector<uint128> tree_indices;
   std::vector<std::pair<int64_t, int>> prefix_map;
   if (num_prefixes > 0)

@@ -344,12 +344,42 @@ class PackedUploads {
   void* event_ = nullptr;
 };
 
+// Orders reuse of a device buffer across calls that may come on different
+// streams: Mark(stream) records an event after the last kernel that touches
+// the buffer; Wait() blocks on it before the next call rewrites the buffer.
+class StreamFence {
+ public:
+  StreamFence() = default;
+  StreamFence(const StreamFence&) = delete;
+  StreamFence& operator=(const StreamFence&) = delete;
+  ~StreamFence() {
+    if (pending_) (void)dpf_hip_event_sync(event_);
+    if (event_) dpf_hip_event_destroy(event_);
+  }
+  Status Wait() {
+    if (pending_) HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
+    pending_ = false;
+    return OkStatus();
+  }
+  Status Mark(void* stream) {
+    if (!event_) HIP_RETURN_IF_ERROR(dpf_hip_event_create(&event_));
+    HIP_RETURN_IF_ERROR(dpf_hip_event_record(event_, stream));
+    pending_ = true;
+    return OkStatus();
+  }
+
+ private:
+  bool pending_ = false;
+  void* event_ = nullptr;
+};
+
 class DeviceScratch {
  public:
   PackedUploads packed;
   DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
   DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;
   DeviceBuffer key_seed, party, block_index, workspace;
+  StreamFence workspace_fence;  // the sum kernels' 192-bit accumulators
   HostStaging staging;
   template <typename T>
   Status Upload(DeviceBuffer& dst, const T* data, size_t count, void* stream = nullptr) {

@@ -382,14 +382,18 @@ Status DistributedPointFunction::EvaluateAtBatchSumToDevice(const DeviceKeyBatch
   if (bad) return InvalidArgumentError("`evaluation_points` larger than the domain size at hierarchy level " +
                                        std::to_string(hierarchy_level));
   auto* s = scratch_.get();
+  // The workspace is zeroed and accumulated into on `stream`: an earlier call
+  // on another stream must have finished with it first.
+  DPF_RETURN_IF_ERROR(s->workspace_fence.Wait());
   DPF_RETURN_IF_ERROR(s->workspace.Reserve(num_points * f.leaves.size() * 3 * sizeof(uint64_t)));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
-  return FromHip(dpf_hip_eval_points_sum(
+  HIP_RETURN_IF_ERROR(dpf_hip_eval_points_sum(
       keys.num_keys(), num_points, L, keys.num_levels(), log_domain_size - L, keys.seed(), keys.party(),
       static_cast<const dpf_block*>(device_points), keys.cw_seed(), keys.cw_left(), keys.cw_right(),
       &kl, &kr, &kv, &desc, keys.value_correction(hierarchy_level), s->workspace.as<uint64_t>(),
       device_out, stream));
+  return s->workspace_fence.Mark(stream);
 }
 
 StatusOr<std::vector<uint8_t>> DistributedPointFunction::SumPackedShares(int hierarchy_level,

@@ -92,9 +92,32 @@ struct Reader {
   }
 };
 
+// Nesting limit of sub-message parses: protobuf's default recursion limit.
+// Value and ValueType nest through their tuples without bound, and keys come
+// from untrusted clients, so deeper input is a parse error, not a stack overflow.
+constexpr int kRecursionLimit = 100;
+thread_local int g_depth = 0;
+thread_local bool g_merge = false;
+
+// First statement of every ParseFromArray: a top-level parse replaces the
+// message; a nested one (a sub-message field, via ParseSub) merges into the
+// field's current value, as protobuf does when a singular message field
+// occurs more than once on the wire.
+template <typename M>
+void BeginParse(M* m) {
+  if (g_merge) g_merge = false;
+  else *m = M();
+}
+
 template <typename M>
 bool ParseSub(Reader r, M* m) {
-  return r.ok && m->ParseFromArray(r.p, static_cast<int>(r.end - r.p));
+  if (!r.ok || g_depth >= kRecursionLimit) return false;
+  ++g_depth;
+  g_merge = true;
+  const bool ok = m->ParseFromArray(r.p, static_cast<int>(r.end - r.p));
+  g_merge = false;
+  --g_depth;
+  return ok;
 }
 
 // Parses a message body: `field(num, wt, reader)` returns false on error.
@@ -148,7 +171,7 @@ bool Block::SerializeToString(std::string* out) const {
   return true;
 }
 bool Block::ParseFromArray(const void* d, int n) {
-  *this = Block();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kVarint) high_ = r.varint();
     else if (f == 2 && wt == kVarint) low_ = r.varint();
@@ -173,7 +196,7 @@ bool Value_Integer::SerializeToString(std::string* out) const {
   return true;
 }
 bool Value_Integer::ParseFromArray(const void* d, int n) {
-  *this = Value_Integer();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kVarint) set_value_uint64(r.varint());
     else if (f == 2 && wt == kLen) return ParseSub(r.len(), mutable_value_uint128());
@@ -199,7 +222,7 @@ bool Value_Tuple::SerializeToString(std::string* out) const {
   return true;
 }
 bool Value_Tuple::ParseFromArray(const void* d, int n) {
-  *this = Value_Tuple();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), add_elements());
     r.skip(wt);
@@ -227,7 +250,7 @@ bool Value::SerializeToString(std::string* out) const {
   return true;
 }
 bool Value::ParseFromArray(const void* d, int n) {
-  *this = Value();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (wt == kLen && f >= 1 && f <= 4) {
       Reader sub = r.len();
@@ -267,7 +290,7 @@ bool ValueType_Integer::SerializeToString(std::string* out) const {
   return true;
 }
 bool ValueType_Integer::ParseFromArray(const void* d, int n) {
-  *this = ValueType_Integer();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kVarint) bitsize_ = static_cast<int32_t>(r.varint());
     else r.skip(wt);
@@ -290,7 +313,7 @@ bool ValueType_Tuple::SerializeToString(std::string* out) const {
   return true;
 }
 bool ValueType_Tuple::ParseFromArray(const void* d, int n) {
-  *this = ValueType_Tuple();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), add_elements());
     r.skip(wt);
@@ -314,7 +337,7 @@ bool ValueType_IntModN::SerializeToString(std::string* out) const {
   return true;
 }
 bool ValueType_IntModN::ParseFromArray(const void* d, int n) {
-  *this = ValueType_IntModN();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_base_integer());
     if (f == 2 && wt == kLen) return ParseSub(r.len(), mutable_modulus());
@@ -345,7 +368,7 @@ bool ValueType::SerializeToString(std::string* out) const {
   return true;
 }
 bool ValueType::ParseFromArray(const void* d, int n) {
-  *this = ValueType();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (wt == kLen && f >= 1 && f <= 4) {
       Reader sub = r.len();
@@ -388,7 +411,7 @@ bool DpfParameters::SerializeToString(std::string* out) const {
   return true;
 }
 bool DpfParameters::ParseFromArray(const void* d, int n) {
-  *this = DpfParameters();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kVarint) log_domain_size_ = static_cast<int32_t>(r.varint());
     else if (f == 3 && wt == kLen) return ParseSub(r.len(), mutable_value_type());
@@ -422,7 +445,7 @@ bool CorrectionWord::SerializeToString(std::string* out) const {
   return true;
 }
 bool CorrectionWord::ParseFromArray(const void* d, int n) {
-  *this = CorrectionWord();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_seed());
     if (f == 2 && wt == kVarint) control_left_ = r.varint() != 0;
@@ -456,7 +479,7 @@ bool DpfKey::SerializeToString(std::string* out) const {
   return true;
 }
 bool DpfKey::ParseFromArray(const void* d, int n) {
-  *this = DpfKey();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_seed());
     if (f == 2 && wt == kLen) return ParseSub(r.len(), add_correction_words());
@@ -489,7 +512,7 @@ bool PartialEvaluation::SerializeToString(std::string* out) const {
   return true;
 }
 bool PartialEvaluation::ParseFromArray(const void* d, int n) {
-  *this = PartialEvaluation();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_prefix());
     if (f == 2 && wt == kLen) return ParseSub(r.len(), mutable_seed());
@@ -522,7 +545,7 @@ bool EvaluationContext::SerializeToString(std::string* out) const {
   return true;
 }
 bool EvaluationContext::ParseFromArray(const void* d, int n) {
-  *this = EvaluationContext();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), add_parameters());
     if (f == 2 && wt == kLen) return ParseSub(r.len(), mutable_key());
@@ -557,7 +580,7 @@ bool DcfParameters::SerializeToString(std::string* out) const {
   return true;
 }
 bool DcfParameters::ParseFromArray(const void* d, int n) {
-  *this = DcfParameters();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_parameters());
     r.skip(wt);
@@ -579,7 +602,7 @@ bool DcfKey::SerializeToString(std::string* out) const {
   return true;
 }
 bool DcfKey::ParseFromArray(const void* d, int n) {
-  *this = DcfKey();
+  BeginParse(this);
   return ParseFields(d, n, [&](int f, int wt, Reader& r) {
     if (f == 1 && wt == kLen) return ParseSub(r.len(), mutable_key());
     r.skip(wt);

@@ -53,6 +53,32 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, device=None) -> list:
+    """Every rank's value of a per-rank scalar, in rank order ([value] without
+    an initialised group)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(value)]
+    t = torch.tensor([float(value)], dtype=torch.float64,
+                     device=device if device is not None else "cpu")
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [float(p.item()) for p in parts]
+
+
+def group_info(kernel_ms: float, device=None) -> dict:
+    """What the process group actually was (world size, backend) and the
+    per-rank dominant-kernel time, for the bench line of every workload."""
+    import torch.distributed as dist
+    up = dist.is_available() and dist.is_initialized()
+    per_rank = gather_over_ranks(kernel_ms, device)
+    return {"world_size": dist.get_world_size() if up else 1,
+            "backend": dist.get_backend() if up else None,
+            "kernel_ms_min": min(per_rank), "kernel_ms_max": max(per_rank),
+            "kernel_ms_per_rank": per_rank}
+
+
 # ---------------------------------------------------------------------------
 # Key-batch sharding (configs 4 and 5, SURVEY.md section 8e)
 # ---------------------------------------------------------------------------
@@ -96,36 +122,56 @@ def _widenable(leaves) -> bool:
                for kind, bits, mod in leaves)
 
 
-def all_reduce_shares(leaves, packed, count: int):
-    """Group sum over ranks via one all_reduce(SUM) of the int64-widened leaves
-    (requires _widenable(leaves)); returns the packed host array."""
-    import numpy as np
+def widen_leaves(leaves, packed, count: int):
+    """[count, num_leaves] int64 tensor of the packed little-endian leaves, built
+    on the tensor's own device (no host round trip): bytes shifted into place
+    and summed (disjoint bit fields, so the sum is the OR; a 64-bit leaf's top
+    byte wraps into the sign bit, which is exact mod 2^64)."""
     import torch
-    import torch.distributed as dist
-    host = packed.cpu().numpy().reshape(count, -1) if hasattr(packed, "cpu") else \
-        np.asarray(packed, np.uint8).reshape(count, -1)
+    rows = packed.reshape(count, -1)
     cols, off = [], 0
     for kind, bits, mod in leaves:
         w = bits // 8
-        raw = np.ascontiguousarray(host[:, off:off + w]).view(f"<u{w}").reshape(count)
-        cols.append(raw.astype(np.uint64).view(np.int64))
+        field = rows[:, off:off + w].to(torch.int64)
+        shifts = torch.arange(0, 8 * w, 8, dtype=torch.int64, device=rows.device)
+        cols.append((field << shifts).sum(dim=1))
         off += w
-    wide = torch.from_numpy(np.stack(cols, axis=1))
-    dev = packed.device if (hasattr(packed, "is_cuda") and packed.is_cuda
-                            and dist.get_backend() != "gloo") else torch.device("cpu")
-    wide = wide.to(dev)
-    dist.all_reduce(wide, op=dist.ReduceOp.SUM)
-    total = wide.cpu().numpy().view(np.uint64)
-    out = np.empty_like(host)
-    off = 0
+    return torch.stack(cols, dim=1)
+
+
+def narrow_leaves(leaves, wide, count: int):
+    """Inverse of widen_leaves after the group reduction: each int64 column
+    reduced mod 2^bits or mod N (IntModN) and packed back into bytes."""
+    import torch
+    parts = []
     for i, (kind, bits, mod) in enumerate(leaves):
+        v = wide[:, i]
+        if kind == "intmodn":
+            v = torch.remainder(v, mod)     # sums of < 2^31 values < 2^32 stay positive
         w = bits // 8
-        v = total[:, i]
-        v = v % np.uint64(mod) if kind == "intmodn" else (
-            v & np.uint64((1 << bits) - 1) if bits < 64 else v)
-        out[:, off:off + w] = v.astype(f"<u{w}").view(np.uint8).reshape(count, w)
-        off += w
-    return out.reshape(-1)
+        shifts = torch.arange(0, 8 * w, 8, dtype=torch.int64, device=v.device)
+        parts.append(((v.unsqueeze(1) >> shifts) & 0xFF).to(torch.uint8))
+    return torch.cat(parts, dim=1).reshape(-1)
+
+
+def all_reduce_shares(leaves, packed, count: int):
+    """Group sum over ranks via one all_reduce(SUM) of the int64-widened leaves
+    (requires _widenable(leaves)).  `packed` is a uint8 tensor on any device;
+    widening, the collective (RCCL when the tensor is on a GPU and the group is
+    NCCL) and the reduction mod 2^bits / N all run on that device, and only the
+    packed result is copied to the host.  A gloo group moves the widened
+    [count, leaves] int64 tensor to the host for the collective, nothing else
+    differs.  Returns the packed host array."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    if not hasattr(packed, "reshape") or isinstance(packed, np.ndarray):
+        packed = torch.from_numpy(np.ascontiguousarray(np.asarray(packed, np.uint8)))
+    wide = widen_leaves(leaves, packed, count)
+    if wide.is_cuda and dist.get_backend() == "gloo":
+        wide = wide.cpu()   # gloo reduces host tensors only
+    dist.all_reduce(wide, op=dist.ReduceOp.SUM)
+    return narrow_leaves(leaves, wide.to(packed.device), count).cpu().numpy()
 
 
 def aggregate_shares(dpf, hierarchy_level: int, packed, count: int):

@@ -20,6 +20,7 @@
 #include "dpf/int_mod_n.h"
 #include "dpf/tuple.h"
 #include "dpf/xor_wrapper.h"
+#include "dpf_hip.h"
 
 namespace dpf = distributed_point_functions;
 using dpf::DistributedPointFunction;
@@ -151,6 +152,48 @@ void Hierarchical() {
   g_checks += 4;
 }
 
+// EvaluateUntilToDevice with a too-small device buffer fails before touching
+// the context, so a retry with the same context and a large enough buffer
+// succeeds and equals EvaluateUntil on a copy of that context.  Covers both
+// the first call (no prefixes) and a prefixed call (partial evaluations).
+void DeviceRetryAfterSmallBuffer() {
+  std::vector<DpfParameters> ps(2);
+  ps[0].set_log_domain_size(4);
+  ps[1].set_log_domain_size(9);
+  for (auto& p : ps) p.mutable_value_type()->mutable_integer()->set_bitsize(64);
+  auto f = Must(DistributedPointFunction::CreateIncremental(ps), "CreateIncremental");
+  auto keys = Must(f->GenerateKeysIncremental(uint128{0x1A5}, {uint128{3}, uint128{5}}),
+                   "GenerateKeysIncremental");
+  EvaluationContext ctx = Must(f->CreateEvaluationContext(keys.first), "ctx");
+  void* dev = nullptr;
+  if (dpf_hip_alloc(&dev, 64 * 8) != 0) Fail("dpf_hip_alloc");
+  std::vector<uint128> none;
+  auto small0 = f->EvaluateUntilToDevice(0, none, ctx, dev, 15 * 8, nullptr);
+  if (small0.ok()) Fail("first call: small buffer accepted");
+  if (ctx.previous_hierarchy_level() != -1) Fail("first call: ctx changed by a failed call");
+  EvaluationContext ref = ctx;
+  std::vector<uint64_t> want0 = Must(f->EvaluateUntil<uint64_t>(0, none, ref), "EvaluateUntil 0");
+  if (Must(f->EvaluateUntilToDevice(0, none, ctx, dev, 16 * 8, nullptr), "retry 0") != 16)
+    Fail("first call: element count");
+  std::vector<uint64_t> got(64);
+  if (dpf_hip_memcpy_d2h(got.data(), dev, 16 * 8, nullptr) != 0) Fail("d2h");
+  for (int i = 0; i < 16; ++i)
+    if (got[i] != want0[i]) Fail("first call: retry output differs");
+  std::vector<uint128> pre = {3, 10};
+  const EvaluationContext before = ctx;
+  auto small1 = f->EvaluateUntilToDevice(1, pre, ctx, dev, 63 * 8, nullptr);
+  if (small1.ok()) Fail("prefixed call: small buffer accepted");
+  if (!(ctx == before)) Fail("prefixed call: ctx changed by a failed call");
+  ref = ctx;
+  std::vector<uint64_t> want1 = Must(f->EvaluateUntil<uint64_t>(1, pre, ref), "EvaluateUntil 1");
+  if (Must(f->EvaluateUntilToDevice(1, pre, ctx, dev, 64 * 8, nullptr), "retry 1") != 64)
+    Fail("prefixed call: element count");
+  if (dpf_hip_memcpy_d2h(got.data(), dev, 64 * 8, nullptr) != 0) Fail("d2h");
+  if (got != want1) Fail("prefixed call: retry output differs");
+  dpf_hip_free(dev);
+  g_checks += 2;
+}
+
 // DCF (dcf/distributed_comparison_function_test.cc): x < alpha -> beta.
 template <typename T>
 void Dcf(int log) {
@@ -189,6 +232,7 @@ int main() {
   FullDomain<dpf::Tuple<uint32_t, uint64_t>>("Tuple<uint32_t, uint64_t>", 22);
   FullDomain<dpf::Tuple<ModN64, ModN64, ModN64>>("Tuple<IntModN64 x3>", 10);
   Hierarchical();
+  DeviceRetryAfterSmallBuffer();
   for (int log : {3, 16, 64}) {
     Dcf<uint32_t>(log);
     Dcf<uint128>(log);

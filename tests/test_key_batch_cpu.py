@@ -194,3 +194,58 @@ def test_serialize_key_batch_roundtrip():
         back = dpf.parse_key_batch(ser, threads=4)
         assert np.array_equal(back.seeds(), b.seeds())
         assert dpf.serialize_key_batch(back, threads=1) == ser
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _len_field(num, payload):
+    return _varint(num << 3 | 2) + _varint(len(payload)) + payload
+
+
+def _key_batch_fixture():
+    levels = [(10, ("int", 16), 0)]
+    dpf = make(levels)
+    rng = np.random.default_rng(6)
+    b0, _ = dpf.generate_key_batch([5, 77], betas_for(levels), root_seeds=seeds_array(rng, 2),
+                                   threads=1)
+    return dpf, [dpf.key_from_batch(b0, k) for k in range(2)]
+
+
+def test_parse_rejects_deep_nesting():
+    # A Value nested ~100k deep through tuples (a few hundred KB from an
+    # untrusted client) is a clean parse error, not a stack overflow: the
+    # parser stops at protobuf's default recursion limit of 100.
+    dpf, keys = _key_batch_fixture()
+    v = b""
+    for _ in range(100_000):
+        v = _len_field(2, _len_field(1, v))          # Value.tuple { elements: v }
+    deep = keys[1].SerializeToString() + _len_field(5, v)
+    with pytest.raises(D.DpfStatusError, match="Failed to parse DpfKey 1"):
+        dpf.parse_key_batch([keys[0].SerializeToString(), deep], threads=1)
+    # 60 levels of nesting (120 message levels) is past the limit as well,
+    # while a shallow nested tuple still parses (then fails validation only).
+    v = b""
+    for _ in range(60):
+        v = _len_field(2, _len_field(1, v))
+    with pytest.raises(D.DpfStatusError, match="Failed to parse DpfKey 0"):
+        dpf.parse_key_batch([keys[0].SerializeToString() + _len_field(5, v)], threads=1)
+
+
+def test_parse_merges_repeated_singular_message():
+    # A singular message field that occurs twice on the wire is merged, as
+    # protobuf does: a second `seed` carrying only `low` keeps the first's `high`.
+    from distributed_point_functions_amd import proto as pb
+    dpf, keys = _key_batch_fixture()
+    raw = keys[0].SerializeToString() + _len_field(1, _varint(2 << 3 | 0) + _varint(12345))
+    want = pb.DpfKey()
+    want.ParseFromString(raw)
+    assert want.seed.low == 12345 and want.seed.high == keys[0].seed.high
+    got = dpf.key_from_batch(dpf.parse_key_batch([raw], threads=1), 0)
+    assert got == want

@@ -106,7 +106,7 @@ VTS = {"intmodn32x2": (("tuple", [("intmodn", 32, 4294967291)] * 2), [[1, 1]]),
        "u128": (("int", 128), [[5]])}   # u128: the all-gather fallback
 
 
-def _key_worker(rank, world, port, q, vt_name="intmodn32x2"):
+def _key_worker(rank, world, port, q, vt_name="intmodn32x2", device="cpu"):
     import torch
     import torch.distributed as dist
     from distributed_point_functions_amd import dpf as D
@@ -131,7 +131,10 @@ def _key_worker(rank, world, port, q, vt_name="intmodn32x2"):
             part = v if part is None else O.add_packed(vt, part, v)
         if part is None:
             part = np.zeros((len(pts), O.packed_size(vt)), np.uint8)
-        total = S.aggregate_shares(dpf, 0, torch.from_numpy(part.reshape(-1).copy()), len(pts))
+        # device="cuda": the partial sums live in HBM as on a GPU rank; widening and
+        # narrowing run there, only the gloo collective itself goes through host.
+        packed = torch.from_numpy(part.reshape(-1).copy()).to(device)
+        total = S.aggregate_shares(dpf, 0, packed, len(pts))
         if rank == 0:
             q.put(total)
         dist.barrier()
@@ -139,15 +142,11 @@ def _key_worker(rank, world, port, q, vt_name="intmodn32x2"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,vt_name", [(2, "intmodn32x2"), (3, "intmodn32x2"), (2, "u64"),
-                                           (3, "u16"), (2, "u128")])
-def test_key_batch_shards_aggregate_to_full_sum(world, vt_name):
-    """all_reduce(SUM) of widened leaves (ints <= 64 bits, IntModN32) or the
-    all-gather fallback (uint128) gives the sum over all keys."""
+def _aggregate_case(world, vt_name, device="cpu"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_key_worker, args=(r, world, port, q, vt_name))
+    procs = [ctx.Process(target=_key_worker, args=(r, world, port, q, vt_name, device))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -165,6 +164,48 @@ def test_key_batch_shards_aggregate_to_full_sum(world, vt_name):
         v = O.evaluate_at(P, O.generate_keys(P, a, beta, 1000 + k, 2000 + k)[k % 2], 0, pts)
         want = v if want is None else O.add_packed(vt, want, v)
     np.testing.assert_array_equal(total.reshape(want.shape), want)
+
+
+@pytest.mark.parametrize("world,vt_name", [(2, "intmodn32x2"), (3, "intmodn32x2"), (2, "u64"),
+                                           (3, "u16"), (2, "u128")])
+def test_key_batch_shards_aggregate_to_full_sum(world, vt_name):
+    """all_reduce(SUM) of widened leaves (ints <= 64 bits, IntModN32) or the
+    all-gather fallback (uint128) gives the sum over all keys."""
+    _aggregate_case(world, vt_name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vt_name", ["intmodn32x2", "u64", "u128"])
+def test_key_batch_aggregate_cuda_tensors(vt_name):
+    """The same aggregation with the partial sums resident on cuda:0 (two gloo
+    ranks share the card): the device-side widen/narrow code that an RCCL
+    group runs, with only the backend differing."""
+    _aggregate_case(2, vt_name, device="cuda:0")
+
+
+def test_widen_narrow_roundtrip():
+    """widen_leaves / narrow_leaves are exact inverses on reduced values, incl.
+    a 64-bit leaf with the top bit set (wraps through int64)."""
+    import torch
+    leaves = [("int", 64, 0), ("intmodn", 32, 4294967291), ("int", 16, 0)]
+    rng = np.random.default_rng(3)
+    rows = np.zeros((5, 14), np.uint8)
+    rows[:, 0:8] = rng.integers(0, 256, size=(5, 8), dtype=np.uint8)
+    rows[0, 7] = 0xFF
+    m = rng.integers(0, 4294967291, size=5, dtype=np.uint64)
+    rows[:, 8:12] = m.astype("<u4").view(np.uint8).reshape(5, 4)
+    rows[:, 12:14] = rng.integers(0, 256, size=(5, 2), dtype=np.uint8)
+    packed = torch.from_numpy(rows.reshape(-1).copy())
+    wide = S.widen_leaves(leaves, packed, 5)
+    assert wide.dtype == torch.int64 and tuple(wide.shape) == (5, 3)
+    assert int(wide[0, 0]) < 0                   # top bit set -> negative int64
+    np.testing.assert_array_equal(S.narrow_leaves(leaves, wide, 5).numpy(), rows.reshape(-1))
+    # doubling then narrowing = the group sum of a row with itself
+    twice = S.narrow_leaves(leaves, wide * 2, 5).numpy().reshape(5, 14)
+    lo = rows[:, 0:8].copy().view("<u8").reshape(5)
+    np.testing.assert_array_equal(twice[:, 0:8].copy().view("<u8").reshape(5), lo * np.uint64(2))
+    np.testing.assert_array_equal(twice[:, 8:12].copy().view("<u4").reshape(5),
+                                  ((m * 2) % 4294967291).astype(np.uint32))
 
 
 def test_key_range_partition():

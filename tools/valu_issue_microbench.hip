@@ -6,6 +6,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 tools/valu_issue_microbench.hip -o tools/bsm_valu
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #define R16(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15)
 
@@ -33,7 +34,23 @@ __global__ __launch_bounds__(256) void k(int iters, uint32_t s, uint32_t* out, u
   if (MODE == 12) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a##i) : "v"(b));                  \
   if (MODE == 13) asm volatile("v_mov_b32 %0, %1" : "=v"(a##i) : "s"(s));                      \
   if (MODE == 14) asm volatile("v_xor_b32_e64 %0, %0, %1" : "+v"(a##i) : "v"(b));              \
-  if (MODE == 15) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(a##i) : "v"(b), "v"(c));
+  if (MODE == 15) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(a##i) : "v"(b), "v"(c));      \
+  if (MODE == 16) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a##i) : "v"(b)); \
+  if (MODE == 17) asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "+v"(a##i) : "v"(b)); \
+  if (MODE == 18) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a##i) : "v"(b), "v"(c));   \
+  if (MODE == 19) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a##i) : "v"(b), "v"(c));      \
+  if (MODE == 20) asm volatile("v_lshl_or_b32 %0, %0, 8, %1" : "+v"(a##i) : "v"(b));           \
+  if (MODE == 21) asm volatile("v_xor_b32 %0, 0x12345678, %0" : "+v"(a##i));                   \
+  if (MODE == 22) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(a##i));                         \
+  if (MODE == 23) asm volatile("v_and_b32 %0, 0xff00, %0" : "+v"(a##i));                       \
+  if (MODE == 24) asm volatile("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a##i) : "v"(b)); \
+  if (MODE == 25) asm volatile("v_xor_b32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(a##i) : "v"(b)); \
+  if (MODE == 26) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));                  \
+  if (MODE == 27) asm volatile("v_lshlrev_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "+v"(a##i) : "v"(b)); \
+  if (MODE == 28) asm volatile("v_and_b32_sdwa %0, %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3 src1_sel:DWORD" : "+v"(a##i) : "v"(b)); \
+  if (MODE == 29) asm volatile("v_mov_b32 %0, %1" : "=v"(a##i) : "v"(b));                       \
+  if (MODE == 30) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a##i) : "v"(b));          \
+  if (MODE == 31) asm volatile("v_lshrrev_b16 %0, 1, %0" : "+v"(a##i));
     R16(OP) R16(OP) R16(OP) R16(OP)
 #undef OP
   }
@@ -43,7 +60,7 @@ __global__ __launch_bounds__(256) void k(int iters, uint32_t s, uint32_t* out, u
   if (threadIdx.x == 0 && blockIdx.x == 0) *clk = t1 - t0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int block = 256, threads = cus * 4 * 64 * 4, iters = 4096;
@@ -57,8 +74,14 @@ int main() {
   const char* names[] = {"v_xor vv", "v_xor sv (VOP2 sgpr)", "bitop3 vvv", "bitop3 vvs",
                          "v_perm vvv", "v_perm vvs", "v_alignbit", "v_lshlrev",
                          "v_lshlrev vv", "v_alignbit vvv", "v_xor inline", "bitop3 0xe4 vvv",
-                         "v_and vv", "v_mov s", "v_xor_e64 vv", "v_bfi vvv"};
-  for (int mode = 0; mode < 16; ++mode) {
+                         "v_and vv", "v_mov s", "v_xor_e64 vv", "v_bfi vvv",
+                         "v_mov_sdwa byte1<-byte2 preserve", "v_or_sdwa byte2", "v_and_or vvv",
+                         "v_or3 vvv", "v_lshl_or v,8,v", "v_xor literal", "v_bfe_u32 const",
+                         "v_and literal", "v_mov_dpp row_shr", "v_xor_dpp quad_perm", "v_add_u32 vv",
+                         "v_lshlrev_sdwa byte2", "v_and_sdwa preserve", "v_mov vv", "v_cndmask vcc",
+                         "v_lshrrev_b16"};
+  int m0 = argc > 1 ? atoi(argv[1]) : 0;
+  for (int mode = m0; mode < 32; ++mode) {
     float best = 1e30f;
     unsigned long long cyc = 0;
     for (int rep = 0; rep < 4; ++rep) {
@@ -66,6 +89,7 @@ int main() {
       switch (mode) {
 #define L(m) case m: k<m><<<threads / block, block>>>(iters, 0x05010400u, d, clk); break;
         L(0) L(1) L(2) L(3) L(4) L(5) L(6) L(7) L(8) L(9) L(10) L(11) L(12) L(13) L(14) L(15)
+        L(16) L(17) L(18) L(19) L(20) L(21) L(22) L(23) L(24) L(25) L(26) L(27) L(28) L(29) L(30) L(31)
 #undef L
       }
       (void)hipEventRecord(b);
