@@ -66,12 +66,16 @@ def parse():
     ap.add_argument("--cpu-chunks", type=int, default=32,
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
     ap.add_argument("--workload", default="full_domain",
-                    choices=["full_domain", "full_domain_u128", "evaluate_at", "evaluate_at_sum",
+                    choices=["full_domain", "full_domain_u128", "full_domain_tuple", "evaluate_at",
+                             "evaluate_at_sum",
                              "synthetic_hierarchical", "synthetic_hierarchical_device",
                              "synthetic_direct", "heavy_hitters", "dcf"],
                     help="full_domain = BASELINE configs[1] (the headline); full_domain_u128 = "
                          "configs[2] (2^31 uint128 outputs per GPU, 2^34 over 8 GPUs); "
                          "evaluate_at(_sum) = configs[3] (2^20 keys x 2^10 points, log 128)")
+    ap.add_argument("--tuple-type", default="intmodn32x2", choices=["intmodn32x2", "u32x2"],
+                    help="full_domain_tuple: Tuple<IntModN<uint32_t, 2^32-5> x 2> (Moller-Granlund "
+                         "sampling from two blocks) or Tuple<uint32_t, uint32_t> (direct)")
     ap.add_argument("--keys-log", type=int, default=20, help="evaluate_at: log2 keys (all ranks)")
     ap.add_argument("--domain", type=int, default=32, help="synthetic_*: log2 domain (32 or 128)")
     ap.add_argument("--distribution", default="uniform", choices=["0.1", "0.5", "uniform"],
@@ -215,6 +219,13 @@ def profiled_traffic(leaves_per_launch: int):
     return best
 
 
+def kernel_name(args, bits: int) -> str:
+    if args.workload == "full_domain_tuple":
+        return ("expand_kernel<Mod32Leaf<2> >" if args.tuple_type == "intmodn32x2"
+                else "expand_kernel<FastIntLeaf<32, false> >")
+    return KERNEL.replace("64", str(bits))
+
+
 def aes_rooflines(achieved: float, kernel: str, **extra) -> dict:
     """`roofline` against the integer-VALU AES roofline (north_star, SURVEY.md
     8d) and `roofline_lds` against the T-table's LDS bound, same achieved rate
@@ -283,11 +294,20 @@ def main():
     log_domain = S.weak_scaling_log_domain(args.log_domain, world)
     params = pb.DpfParameters()
     params.log_domain_size = log_domain
-    params.value_type.CopyFrom(D.integer_type(bits))
+    if args.workload == "full_domain_tuple":
+        # Tuple leaves: both types pack to 8 bytes.
+        if args.tuple_type == "intmodn32x2":
+            el = D.int_mod_n_type(32, 4294967291)
+            vtype, beta_py = D.tuple_type(el, el), (123456789, 4000000000)
+        else:
+            vtype, beta_py = D.tuple_type(D.integer_type(32), D.integer_type(32)), (0xDEADBEEF, 7)
+    else:
+        vtype, beta_py = D.integer_type(bits), 0xDEADBEEF
+    params.value_type.CopyFrom(vtype)
     dpf = D.DistributedPointFunction.create(params)
     # Same key on every rank: root seeds injected (GenerateKeysIncrementalWithSeeds).
     alpha = 0x2545F4914F6CDD1D % (1 << log_domain)
-    beta = D.to_value(D.integer_type(bits), 0xDEADBEEF)
+    beta = D.to_value(vtype, beta_py)
     key, _ = dpf.generate_keys_incremental(alpha, [beta], seeds=(0x243F6A8885A308D3,
                                                                  0x13198A2E03707344))
     ctx0 = dpf.create_evaluation_context(key)
@@ -328,15 +348,28 @@ def main():
     # at alpha, 0 elsewhere) on a few positions of this rank's shard.
     _check_shard(dpf, key, out, rank, world, outputs_per_rank, alpha, bits)
 
-    aes_per_launch = tree_aes_per_launch(depth)
+    # Value hashes per leaf: the blocks the conversion reads (b = 1 for
+    # integers and direct tuples; 2 for Tuple<IntModN32 x 2>: 16 + 4 bytes
+    # sampled, value_type_helpers.h:415-443).  The reference hashes
+    # blocks_needed blocks per leaf (HashExpandedSeeds, cc:500-524).
+    tuple_mod = args.workload == "full_domain_tuple" and args.tuple_type == "intmodn32x2"
+    b_read = 2 if tuple_mod else 1
+    aes_per_launch = tree_aes_per_launch(depth, b_read)
+    ref_aes_per_launch = tree_aes_per_launch(depth, dpf.blocks_needed(0))
     achieved = aes_per_launch / (kern_ms_max * 1e-3) / 1e9
     bytes_per_launch = outputs_per_rank * esz
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = profiled_traffic(outputs_per_rank) if bits == 64 else None
+        tr = profiled_traffic(outputs_per_rank) if args.workload == "full_domain" else None
+        vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
+                 "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "
+                                                      "IntModN<uint32_t, 4294967291>>",
+                                       "u32x2": "Tuple<uint32_t, uint32_t>"}[args.tuple_type]
+                 }[args.workload]
         res = {
-            "metric": METRIC,
+            "metric": METRIC if args.workload == "full_domain" else
+                      f"DPF leaf evals/sec, full-domain {vname}; AES blocks/s",
             "value": total / elapsed,
             "unit": "leaves/s",
             "n_gpus": world,
@@ -346,16 +379,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": f"u{bits}",
+            "dtype": "u32 mod N" if tuple_mod else ("u32" if args.workload == "full_domain_tuple"
+                                                   else f"u{bits}"),
             "data": "synthetic: one DpfKey from the product keygen with fixed root seeds",
+            "reference_aes_blocks_per_launch": ref_aes_per_launch,
             "config": {"workload": f"full-domain EvaluateUntil(0, {{}}) of one key, "
-                                   f"log_domain_size={log_domain}, uint{bits}, 2^{args.log_domain} "
+                                   f"log_domain_size={log_domain}, {vname}, 2^{args.log_domain} "
                                    f"outputs per GPU",
-                       "log_domain_size": log_domain, "value_type": f"uint{bits}",
+                       "log_domain_size": log_domain, "value_type": vname,
+                       "blocks_needed": dpf.blocks_needed(0), "value_blocks_hashed_per_leaf": b_read,
                        "outputs_per_gpu": outputs_per_rank, "tree_levels_per_gpu": depth,
                        "parallelism": f"subtree-prefix x{world}"},
             "aes_blocks_per_s": aes_per_launch * world * args.steps / elapsed,
-            **aes_rooflines(achieved, KERNEL.replace("64", str(bits)),
+            **aes_rooflines(achieved, kernel_name(args, bits),
                             traffic=tr[0] if tr else None,
                             traffic_source=tr[1] if tr else None,
                             pmc=tr[2] if tr else None, launch_ms=kern_ms_max,
@@ -367,7 +403,7 @@ def main():
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload != "full_domain_tuple":
             res["cpu_baseline"] = cpu_baseline(key, log_domain, args.cpu_chunks, bits)
         print(json.dumps(res), flush=True)
     if world > 1:

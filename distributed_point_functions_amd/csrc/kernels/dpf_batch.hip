@@ -39,47 +39,6 @@ using namespace dpf_rt;
 
 namespace {
 
-constexpr int kMod32MaxLeaves = 4;
-
-// Invariant-divisor division of a 64-bit value by a 32-bit modulus
-// (Moller & Granlund, "Improved division by invariant integers", Alg. 4):
-// dn = N << sh is normalised (top bit set) and v = floor((2^64-1)/dn) - 2^32.
-struct Div32 {
-  uint32_t dn, v;
-  int sh;
-  uint32_t n;
-};
-
-// (u1:u0) / d for u1 < d, d normalised.  Returns the quotient word, r = remainder.
-__device__ __forceinline__ uint32_t div_2by1(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v,
-                                             uint32_t& r) {
-  uint64_t q = (uint64_t)v * u1;
-  q += ((uint64_t)(u1 + 1u) << 32) | u0;
-  uint32_t q1 = (uint32_t)(q >> 32), q0 = (uint32_t)q;
-  uint32_t rr = u0 - q1 * d;
-  if (rr > q0) { --q1; rr += d; }
-  if (rr >= d) { ++q1; rr -= d; }
-  r = rr;
-  return q1;
-}
-
-// 128-bit block w (little-endian words) -> remainder mod N, and the low three
-// quotient words (what `quotient << 32` keeps of it, int_mod_n.h:167-176).
-__device__ __forceinline__ uint32_t divmod128(const uint32_t w[4], const Div32& d, uint32_t q[3]) {
-  const int sh = d.sh;
-  uint32_t u4 = sh ? (w[3] >> (32 - sh)) : 0u;
-  uint32_t u3 = (w[3] << sh) | (sh ? (w[2] >> (32 - sh)) : 0u);
-  uint32_t u2 = (w[2] << sh) | (sh ? (w[1] >> (32 - sh)) : 0u);
-  uint32_t u1 = (w[1] << sh) | (sh ? (w[0] >> (32 - sh)) : 0u);
-  uint32_t u0 = w[0] << sh;
-  uint32_t r = u4;
-  (void)div_2by1(r, u3, d.dn, d.v, r);  // top quotient word: shifted out by `<< 32`
-  q[2] = div_2by1(r, u2, d.dn, d.v, r);
-  q[1] = div_2by1(r, u1, d.dn, d.v, r);
-  q[0] = div_2by1(r, u0, d.dn, d.v, r);
-  return r >> sh;
-}
-
 struct BatchLevelParams {
   int64_t num_keys;
   int64_t num_starts;       // U
@@ -582,28 +541,6 @@ __global__ void gather_batched_kernel(int64_t keys, int64_t in_row, int64_t rows
     const int64_t r = rem / row_bytes, c = rem - r * row_bytes;
     out[i] = in[(k * in_row + src[r]) * elem_size + c];
   }
-}
-
-Div32 make_div32(uint32_t n) {
-  Div32 d;
-  d.n = n;
-  d.sh = __builtin_clz(n);
-  d.dn = n << d.sh;
-  d.v = (uint32_t)(~0ull / d.dn - (1ull << 32));
-  return d;
-}
-
-// Tuples of IntModN<uint32_t, N < 2^32> sampled from <= 2 blocks.
-bool mod32_eligible(const dpf_value_desc* d, int* blocks_read) {
-  if (d->direct || d->elements_per_block != 1 || d->num_leaves > kMod32MaxLeaves) return false;
-  for (int k = 0; k < d->num_leaves; ++k)
-    if (d->kind[k] != DPF_LEAF_INTMODN || d->bits[k] != 32 || d->mod_high[k] != 0 ||
-        d->mod_low[k] == 0 || d->mod_low[k] > 0xffffffffull)
-      return false;
-  const int bytes = 16 + 4 * (d->num_leaves - 1);
-  if (bytes > 16 * d->blocks_needed) return false;
-  *blocks_read = (bytes + 15) / 16;
-  return true;
 }
 
 template <class V, int MAXE, bool SUM>

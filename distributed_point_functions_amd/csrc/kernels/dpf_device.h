@@ -100,13 +100,27 @@ __device__ __forceinline__ void fill_cws(LdsImage& lds, const dpf_block* cw_seed
 // builds the byte address {lane offset, byte K of w, table half, 0}, i.e.
 // (entry << 8) | lt[T] with lt[T] = (lane & 31) * 4 (+128 for T1/T3, +64 KiB
 // for T2/T3).
+//
+// Byte 1 of w already sits at bits 8-15, where the address wants it: that
+// lookup's address is (w & 0xff00) | lt[T], one v_bitop3_b32 -- a full-rate
+// VALU op, where v_perm_b32 is half rate (profiles/r10_valu_issue_microbench.txt)
+// -- with the mask held in a VGPR (an SGPR operand would make it half rate too).
 struct LdsLookup {
   const char* base;
   uint32_t lt[4];
+  uint32_t m1;  // 0xff00 in a VGPR
   template <int T, int K>
   __device__ __forceinline__ uint32_t lookup(uint32_t w) const {
-    constexpr uint32_t sel = 0x0c020000u | ((4u + K) << 8);
-    uint32_t off = __builtin_amdgcn_perm(w, lt[T], sel);
+    uint32_t off;
+#if !defined(DPF_NO_BYTE1_BITOP3)
+    if constexpr (K == 1) {
+      off = __builtin_amdgcn_bitop3_b32(w, m1, lt[T], 0xEA);  // (S0 & S1) | S2
+    } else
+#endif
+    {
+      constexpr uint32_t sel = 0x0c020000u | ((4u + K) << 8);
+      off = __builtin_amdgcn_perm(w, lt[T], sel);
+    }
     return *reinterpret_cast<const uint32_t*>(base + off);
   }
   __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) const {
@@ -116,7 +130,10 @@ struct LdsLookup {
 
 __device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds) {
   uint32_t l = (threadIdx.x & 31) * 4u;
-  return LdsLookup{reinterpret_cast<const char*>(lds.tab), {l, l + 128u, l + 65536u, l + 65664u}};
+  uint32_t m1;
+  asm volatile("v_mov_b32 %0, 0xff00" : "=v"(m1));
+  return LdsLookup{reinterpret_cast<const char*>(lds.tab), {l, l + 128u, l + 65536u, l + 65664u},
+                   m1};
 }
 
 // Round keys shared by the whole wave (kernel-argument resident).
@@ -145,6 +162,27 @@ struct SelectRK {
 };
 
 using dpf_aes::Block4;
+using u128 = unsigned __int128;
+
+__device__ __forceinline__ u128 block_u128(Block4 h) {
+  return ((u128)h.w3 << 96) | ((u128)h.w2 << 64) | ((u128)h.w1 << 32) | h.w0;
+}
+__device__ __forceinline__ u128 dpf_u128(dpf_block c) { return ((u128)c.high << 64) | c.low; }
+
+// Full-domain expansion launch (dpf_hip_expand): items are subtrees.
+struct ExpandParams {
+  int64_t num_items;  // num_starts << k0
+  int num_levels;     // L = k0 + S
+  int k0;             // levels walked per item (per-lane direction)
+  int S;              // subtree depth visited per item
+  const dpf_block* seeds_in;
+  const uint8_t* ctrl_in;
+  const dpf_block* cw_seed;
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  char* out;
+  RoundKeys rkl, rkr, rkv, rkd;
+};
 
 __device__ __forceinline__ Block4 load_block(const dpf_block* p) {
   uint4 v = *reinterpret_cast<const uint4*>(p);
@@ -271,6 +309,27 @@ __device__ __forceinline__ Block4 lanes_neg(Block4 a) {
   }
 }
 
+// Stores `bytes` (1..16) of a little-endian 128-bit value with the widest
+// stores the alignment of `p` (a multiple of the packed element size) allows.
+__device__ __forceinline__ void store_packed(char* p, Block4 v, int bytes) {
+  switch (bytes) {
+    case 16: *reinterpret_cast<uint4*>(p) = make_uint4(v.w0, v.w1, v.w2, v.w3); return;
+    case 8: *reinterpret_cast<uint2*>(p) = make_uint2(v.w0, v.w1); return;
+    case 4: *reinterpret_cast<uint32_t*>(p) = v.w0; return;
+    case 2: *reinterpret_cast<uint16_t*>(p) = (uint16_t)v.w0; return;
+    case 1: *reinterpret_cast<uint8_t*>(p) = (uint8_t)v.w0; return;
+    case 12: {
+      uint32_t* q = reinterpret_cast<uint32_t*>(p);
+      q[0] = v.w0; q[1] = v.w1; q[2] = v.w2;
+      return;
+    }
+    default: {
+      const uint32_t w[4] = {v.w0, v.w1, v.w2, v.w3};
+      for (int i = 0; i < bytes; ++i) p[i] = (char)(uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    }
+  }
+}
+
 // Plain unsigned integers and XorWrapper of them with b == 1: the hashed block
 // *is* the element array (value_type_helpers.h:199-211), the correction word is
 // one block in the same layout.
@@ -312,14 +371,7 @@ struct FastIntLeaf {
   }
 
   __device__ __forceinline__ void store(Block4 h, int64_t leaf, char* out) const {
-    char* p = out + leaf * (int64_t)store_bytes;
-    switch (store_bytes) {
-      case 16: *reinterpret_cast<uint4*>(p) = make_uint4(h.w0, h.w1, h.w2, h.w3); break;
-      case 8: *reinterpret_cast<uint2*>(p) = make_uint2(h.w0, h.w1); break;
-      case 4: *reinterpret_cast<uint32_t*>(p) = h.w0; break;
-      case 2: *reinterpret_cast<uint16_t*>(p) = (uint16_t)h.w0; break;
-      default: *reinterpret_cast<uint8_t*>(p) = (uint8_t)h.w0; break;
-    }
+    store_packed(out + leaf * (int64_t)store_bytes, h, store_bytes);
   }
 
   // Full-domain leaf: write elements_per_leaf elements.
@@ -358,6 +410,224 @@ struct FastIntLeaf {
 #pragma unroll
       for (int i = 0; i < 4; ++i) store(s[i], leaf + i, out);
     }
+  }
+};
+
+// Invariant-divisor division of a 64-bit value by a 32-bit modulus
+// (Moller & Granlund, "Improved division by invariant integers", Alg. 4):
+// dn = N << sh is normalised (top bit set) and v = floor((2^64-1)/dn) - 2^32.
+struct Div32 {
+  uint32_t dn, v;
+  int sh;
+  uint32_t n;
+};
+
+// (u1:u0) / d for u1 < d, d normalised.  Returns the quotient word, r = remainder.
+__device__ __forceinline__ uint32_t div_2by1(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v,
+                                             uint32_t& r) {
+  uint64_t q = (uint64_t)v * u1;
+  q += ((uint64_t)(u1 + 1u) << 32) | u0;
+  uint32_t q1 = (uint32_t)(q >> 32), q0 = (uint32_t)q;
+  uint32_t rr = u0 - q1 * d;
+  if (rr > q0) { --q1; rr += d; }
+  if (rr >= d) { ++q1; rr -= d; }
+  r = rr;
+  return q1;
+}
+
+// 128-bit block w (little-endian words) -> remainder mod N, and the low three
+// quotient words (what `quotient << 32` keeps of it, int_mod_n.h:167-176).
+__device__ __forceinline__ uint32_t divmod128(const uint32_t w[4], const Div32& d, uint32_t q[3]) {
+  const int sh = d.sh;
+  uint32_t u4 = sh ? (w[3] >> (32 - sh)) : 0u;
+  uint32_t u3 = (w[3] << sh) | (sh ? (w[2] >> (32 - sh)) : 0u);
+  uint32_t u2 = (w[2] << sh) | (sh ? (w[1] >> (32 - sh)) : 0u);
+  uint32_t u1 = (w[1] << sh) | (sh ? (w[0] >> (32 - sh)) : 0u);
+  uint32_t u0 = w[0] << sh;
+  uint32_t r = u4;
+  (void)div_2by1(r, u3, d.dn, d.v, r);  // top quotient word: shifted out by `<< 32`
+  q[2] = div_2by1(r, u2, d.dn, d.v, r);
+  q[1] = div_2by1(r, u1, d.dn, d.v, r);
+  q[0] = div_2by1(r, u0, d.dn, d.v, r);
+  return r >> sh;
+}
+
+
+inline Div32 make_div32(uint32_t n) {
+  Div32 d;
+  d.n = n;
+  d.sh = __builtin_clz(n);
+  d.dn = n << d.sh;
+  d.v = (uint32_t)(~0ull / d.dn - (1ull << 32));
+  return d;
+}
+
+
+
+// Tuples of IntModN<uint32_t, N < 2^32> sampled from <= 2 blocks.
+constexpr int kMod32MaxLeaves = 4;
+inline bool mod32_eligible(const dpf_value_desc* d, int* blocks_read) {
+  if (d->direct || d->elements_per_block != 1 || d->num_leaves > kMod32MaxLeaves) return false;
+  for (int k = 0; k < d->num_leaves; ++k)
+    if (d->kind[k] != DPF_LEAF_INTMODN || d->bits[k] != 32 || d->mod_high[k] != 0 ||
+        d->mod_low[k] == 0 || d->mod_low[k] > 0xffffffffull)
+      return false;
+  const int bytes = 16 + 4 * (d->num_leaves - 1);
+  if (bytes > 16 * d->blocks_needed) return false;
+  *blocks_read = (bytes + 15) / 16;
+  return true;
+}
+
+// Direct conversion of a tuple of plain integers / XorWrappers of MIXED widths
+// (value_type_helpers.h:199-211, 286-311 with CanBeConvertedDirectly): the
+// hashed block is E packed elements, each the concatenation of its leaves, so
+// the correction is a lane-wise add (XOR for XorWrapper lanes) on the 128-bit
+// block with lanes of the leaves' widths -- SWAR on one u128: carries stop at
+// the lane top bits `top`, XorWrapper lanes (`xmask`) take a ^ b.  Tuples whose
+// leaves all have one width and kind go to FastIntLeaf instead.
+struct SwarLeaf {
+  const dpf_block* vcw_elems;  // lanes = E * num_leaves values (device)
+  int lanes;
+  int party;
+  int store_bytes;             // elements_per_leaf * packed element size
+  uint8_t lane_off[16];        // bit offset of lane i in the block (lanes <= 16)
+  uint8_t lane_bits[16];
+  u128 top, xmask;             // lane top bits (all lanes) / XorWrapper lane bits
+  u128 vcw;                    // packed correction, set by init
+
+  __device__ __forceinline__ void init() {
+    u128 packed = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // unrolled: no dynamic index into the struct
+      if (i < lanes) {
+        const int b = lane_bits[i];
+        u128 v = dpf_u128(vcw_elems[i]);
+        if (b < 128) v &= (((u128)1 << b) - 1);
+        packed |= v << (lane_off[i] & 127);
+      }
+    }
+    vcw = packed;
+  }
+  __device__ __forceinline__ u128 add(u128 a, u128 b) const {
+    const u128 s = ((a & ~top) + (b & ~top)) ^ ((a ^ b) & top);
+    return (s & ~xmask) | ((a ^ b) & xmask);
+  }
+  __device__ __forceinline__ u128 neg(u128 a) const {
+    const u128 n = (top - (a & ~top)) ^ (~a & top);
+    return (n & ~xmask) | (a & xmask);
+  }
+  __device__ __forceinline__ Block4 correct(Block4 h, uint32_t t) const {
+    u128 x = block_u128(h);
+    if (t) x = add(x, vcw);
+    if (party == 1) x = neg(x);
+    return Block4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
+  }
+  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+                                       uint32_t t, int64_t leaf, char* out) const {
+    store_packed(out + leaf * (int64_t)store_bytes,
+                 correct(dpf_aes::mmo_hash(seed, lk, UniformRK{rkv}), t), store_bytes);
+  }
+  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+                                        uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
+                                        char* out) const {
+    dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{rkv}, UniformRK{rkv});
+    store_packed(out + leaf * (int64_t)store_bytes, correct(s0, t0), store_bytes);
+    store_packed(out + (leaf + 1) * (int64_t)store_bytes, correct(s1, t1), store_bytes);
+  }
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+                                        const uint32_t* t, int64_t leaf, char* out) const {
+    emit2(lk, rkv, s[0], t[0], s[1], t[1], leaf, out);
+    emit2(lk, rkv, s[2], t[2], s[3], t[3], leaf + 2, out);
+  }
+};
+
+// Tuples of IntModN<uint32_t, N_i < 2^32> (and a single IntModN<uint32_t, N>),
+// full domain (E == 1): sampled from the first `b` hashed blocks of seed, seed+1
+// (value_type_helpers.h:415-443, int_mod_n.h:155-177): r = the first 16 bytes;
+// value_i = r mod N_i; r = (r / N_i) << 32 | the next 4 bytes.  Division by
+// the invariant N_i is Div32's 2-by-1 word algorithm (no 128-bit division);
+// only the b <= 2 blocks the sampling reads are hashed (blocks_needed may be
+// more: the bytes past them never reach an output).
+template <int NLMAX>
+struct Mod32Leaf {
+  const dpf_block* vcw_elems;  // num_leaves values (E == 1)
+  int nl;
+  int b;                       // hashed blocks read by the sampling: 1 or 2
+  int party;
+  Div32 div[NLMAX];
+  uint32_t c[NLMAX];           // value correction per leaf, set by init
+
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < NLMAX; ++i) c[i] = i < nl ? (uint32_t)vcw_elems[i].low : 0u;
+  }
+  __device__ __forceinline__ void convert_store(const uint32_t* w, uint32_t t, char* o) const {
+    uint32_t blk[4] = {w[0], w[1], w[2], w[3]};
+    uint32_t x[NLMAX];
+#pragma unroll
+    for (int i = 0; i < NLMAX; ++i) {
+      if (i < nl) {
+        uint32_t q[3];
+        const uint32_t n = div[i].n;
+        uint32_t r = divmod128(blk, div[i], q);
+        if (t) {  // IntModN += (int_mod_n.h:116-120)
+          const uint32_t s = r + c[i];
+          r = (s < r || s >= n) ? s - n : s;
+        }
+        if (party == 1) r = r == 0 ? 0u : n - r;
+        x[i] = r;
+        blk[0] = w[4 + i]; blk[1] = q[0]; blk[2] = q[1]; blk[3] = q[2];
+      }
+    }
+    if (NLMAX >= 2 && nl == 2) {
+      *reinterpret_cast<uint2*>(o) = make_uint2(x[0], x[NLMAX >= 2 ? 1 : 0]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NLMAX; ++i)
+        if (i < nl) reinterpret_cast<uint32_t*>(o)[i] = x[i];
+    }
+  }
+  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+                                       uint32_t t, int64_t leaf, char* out) const {
+    uint32_t w[8];
+    Block4 h0 = seed, h1 = add_small(seed, 1u);
+    if (b == 2) {
+      dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{rkv}, UniformRK{rkv});
+    } else {
+      h0 = dpf_aes::mmo_hash(h0, lk, UniformRK{rkv});
+      h1 = Block4{0, 0, 0, 0};
+    }
+    w[0] = h0.w0; w[1] = h0.w1; w[2] = h0.w2; w[3] = h0.w3;
+    w[4] = h1.w0; w[5] = h1.w1; w[6] = h1.w2; w[7] = h1.w3;
+    convert_store(w, t, out + leaf * 4 * nl);
+  }
+  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+                                        uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
+                                        char* out) const {
+    uint32_t w0[8], w1[8];
+    if (b == 2) {
+      // Both leaves' two blocks (seed, seed + 1) as one interleaved quadruple.
+      Block4 h[4] = {s0, add_small(s0, 1u), s1, add_small(s1, 1u)};
+      const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
+      dpf_aes::mmo_hashN<4>(h, lk, rk);
+      w0[0] = h[0].w0; w0[1] = h[0].w1; w0[2] = h[0].w2; w0[3] = h[0].w3;
+      w0[4] = h[1].w0; w0[5] = h[1].w1; w0[6] = h[1].w2; w0[7] = h[1].w3;
+      w1[0] = h[2].w0; w1[1] = h[2].w1; w1[2] = h[2].w2; w1[3] = h[2].w3;
+      w1[4] = h[3].w0; w1[5] = h[3].w1; w1[6] = h[3].w2; w1[7] = h[3].w3;
+    } else {
+      dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{rkv}, UniformRK{rkv});
+      w0[0] = s0.w0; w0[1] = s0.w1; w0[2] = s0.w2; w0[3] = s0.w3;
+      w1[0] = s1.w0; w1[1] = s1.w1; w1[2] = s1.w2; w1[3] = s1.w3;
+#pragma unroll
+      for (int i = 4; i < 8; ++i) w0[i] = w1[i] = 0;
+    }
+    convert_store(w0, t0, out + leaf * 4 * nl);
+    convert_store(w1, t1, out + (leaf + 1) * 4 * nl);
+  }
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+                                        const uint32_t* t, int64_t leaf, char* out) const {
+    emit2(lk, rkv, s[0], t[0], s[1], t[1], leaf, out);
+    emit2(lk, rkv, s[2], t[2], s[3], t[3], leaf + 2, out);
   }
 };
 
@@ -508,12 +778,6 @@ __device__ __forceinline__ void path_step2(const LdsLookup& lk, const RoundKeys&
   s1 = h1; t1 = n1;
 }
 
-using u128 = unsigned __int128;
-
-__device__ __forceinline__ u128 block_u128(Block4 h) {
-  return ((u128)h.w3 << 96) | ((u128)h.w2 << 64) | ((u128)h.w1 << 32) | h.w0;
-}
-__device__ __forceinline__ u128 dpf_u128(dpf_block c) { return ((u128)c.high << 64) | c.low; }
 
 // Element `bi` of a directly converted integer block, corrected and negated
 // (distributed_point_function.h:993-1002; value_type_helpers.h:199-211).

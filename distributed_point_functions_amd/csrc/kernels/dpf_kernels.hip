@@ -102,20 +102,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_paths_kernel(PathP
   }
 }
 
-struct ExpandParams {
-  int64_t num_items;  // num_starts << k0
-  int num_levels;     // L = k0 + S
-  int k0;             // levels walked per item (per-lane direction)
-  int S;              // subtree depth visited depth-first per item
-  const dpf_block* seeds_in;
-  const uint8_t* ctrl_in;
-  const dpf_block* cw_seed;
-  const uint8_t* cw_left;
-  const uint8_t* cw_right;
-  char* out;
-  RoundKeys rkl, rkr, rkv, rkd;
-};
-
 template <class Leaf>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandParams p, Leaf leaf) {
   __shared__ LdsImage lds;
@@ -829,6 +815,10 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
     return fail(kInvalidArgument, "NULL pointer");
   if (num_starts > (INT64_MAX >> num_levels))
     return fail(kInvalidArgument, "expansion too large");
+  if (expand_hybrid_applies(num_starts, num_levels, key_value, desc, elements_per_leaf))
+    return launch_expand_hybrid(num_starts, seeds_in, control_in, num_levels, cw_seed, cw_left,
+                                cw_right, key_left, key_right, key_value, desc, value_correction,
+                                party, out, (hipStream_t)stream);
   // Choose the depth-first subtree depth S and the per-item walk depth k0.
   const int64_t threads = (int64_t)num_cus() * kWgPerCu * kBlock;
   int S = num_levels < kSMax ? num_levels : kSMax;
@@ -865,12 +855,71 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       default: return launch_expand_fast<128>(p, desc, value_correction, E, party, store_bytes, s);
     }
   }
+  const int esz = packed_size(desc);
+  if (desc->direct && desc->blocks_needed == 1) {
+    // Direct tuples of plain integers / XorWrappers: the hashed block is E
+    // packed elements (value_type_helpers.h:199-211).
+    const int nl = desc->num_leaves, bits = desc->bits[0], kind = desc->kind[0];
+    bool uniform = true;
+    for (int k = 1; k < nl; ++k) uniform = uniform && desc->bits[k] == bits && desc->kind[k] == kind;
+    const int lanes = desc->elements_per_block * nl;
+    if (uniform && lanes * bits <= 128) {
+      // Every lane the same width and kind: the integer fast path with E * nl lanes.
+      const int store_bytes = elements_per_leaf * esz;
+      switch (bits) {
+        case 8: return launch_expand_fast<8>(p, desc, value_correction, lanes, party, store_bytes, s);
+        case 16: return launch_expand_fast<16>(p, desc, value_correction, lanes, party, store_bytes, s);
+        case 32: return launch_expand_fast<32>(p, desc, value_correction, lanes, party, store_bytes, s);
+        case 64: return launch_expand_fast<64>(p, desc, value_correction, lanes, party, store_bytes, s);
+        default: return launch_expand_fast<128>(p, desc, value_correction, lanes, party, store_bytes, s);
+      }
+    }
+    if (lanes <= 16 && desc->elements_per_block * esz <= 16) {
+      SwarLeaf w;
+      memset(&w, 0, sizeof(w));
+      w.vcw_elems = value_correction;
+      w.lanes = lanes;
+      w.party = party;
+      w.store_bytes = elements_per_leaf * esz;
+      int off = 0;
+      for (int i = 0; i < lanes; ++i) {
+        const int b = desc->bits[i % nl];
+        w.lane_off[i] = (uint8_t)off;
+        w.lane_bits[i] = (uint8_t)b;
+        w.top |= (u128)1 << (off + b - 1);
+        if (desc->kind[i % nl] == DPF_LEAF_XOR)
+          w.xmask |= (b >= 128 ? ~(u128)0 : (((u128)1 << b) - 1)) << off;
+        off += b;
+      }
+      return launch_expand(p, w, s);
+    }
+  }
+  int b = 0;
+  if (elements_per_leaf == 1 && mod32_eligible(desc, &b)) {
+    // Tuples of IntModN<uint32_t, N>: Moller-Granlund sampling.
+    auto fill = [&](auto& m) {
+      memset(&m, 0, sizeof(m));
+      m.vcw_elems = value_correction;
+      m.nl = desc->num_leaves;
+      m.b = b;
+      m.party = party;
+      for (int k = 0; k < desc->num_leaves; ++k) m.div[k] = make_div32((uint32_t)desc->mod_low[k]);
+    };
+    if (desc->num_leaves <= 2) {
+      Mod32Leaf<2> m;
+      fill(m);
+      return launch_expand(p, m, s);
+    }
+    Mod32Leaf<kMod32MaxLeaves> m;
+    fill(m);
+    return launch_expand(p, m, s);
+  }
   GenericLeaf g;
   g.d = *desc;
   g.vcw = value_correction;
   g.party = party;
   g.elements_per_leaf = elements_per_leaf;
-  g.esz = packed_size(desc);
+  g.esz = esz;
   return launch_expand(p, g, s);
 }
 

@@ -10,6 +10,13 @@
 #include "../../distributed_point_functions_amd/csrc/kernels/bs_aes.h"
 
 static int g_bad = 0;
+
+// The value PRG key (distributed_point_function.cc:37-42) as a memory image.
+static constexpr uint8_t kv[16] = {0x98, 0x1c, 0x1d, 0xb2, 0x01, 0x11, 0xa3, 0x46,
+                                   0xe3, 0x23, 0x54, 0x8c, 0x58, 0xd1, 0xa5, 0x05};
+struct KM {
+  static constexpr bsa::BsKeyMasks m = bsa::make_key_masks_c(kv);
+};
 #define CHECK(c, ...)                  \
   do {                                 \
     if (!(c)) {                        \
@@ -80,6 +87,31 @@ int main() {
       bsa::mmo8(w, bsa::ArrayMasks{km.m});
       CHECK(!memcmp(w, ref, sizeof w), "mmo8 vs T-table, key %016llx, it %d",
             (unsigned long long)k[0], it);
+    }
+  }
+  // 4. Compile-time masks (make_key_masks_c) equal the run-time ones, and the
+  //    unrolled literal-mask AES (aes8_c, used by dpf_expand_hybrid.hip) plus
+  //    the MMO feed-forward equals the T-table hash under the value PRG key.
+  {
+    uint32_t rk[44];
+    dpf_aes::expand_key(kv, rk);
+    const bsa::BsKeyMasks km = bsa::make_key_masks(rk);
+    CHECK(!memcmp(km.m, KM::m.m, sizeof km.m), "constexpr key masks");
+    for (int it = 0; it < 64; ++it) {
+      uint32_t w[32], ref[32], sg[32];
+      for (auto& v : w) v = (uint32_t)rng();
+      for (int b = 0; b < 8; ++b) {
+        dpf_aes::Block4 x{w[4 * b], w[4 * b + 1], w[4 * b + 2], w[4 * b + 3]};
+        dpf_aes::Block4 h = dpf_aes::mmo_hash(x, lk, dpf_aes::ArrayRK{rk});
+        ref[4 * b] = h.w0; ref[4 * b + 1] = h.w1; ref[4 * b + 2] = h.w2; ref[4 * b + 3] = h.w3;
+        dpf_aes::Block4 s = dpf_aes::sigma(x);
+        sg[4 * b] = s.w0; sg[4 * b + 1] = s.w1; sg[4 * b + 2] = s.w2; sg[4 * b + 3] = s.w3;
+      }
+      uint32_t e[32];
+      memcpy(e, sg, sizeof e);
+      bsa::aes8_c<KM>(e);
+      for (int j = 0; j < 32; ++j) e[j] ^= sg[j];
+      CHECK(!memcmp(e, ref, sizeof e), "aes8_c + feed-forward vs T-table, it %d", it);
     }
   }
   printf("bs_aes_test: %d failures\n", g_bad);

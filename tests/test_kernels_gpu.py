@@ -152,6 +152,48 @@ def test_expand_fast_types(hip, vt, levels, n0, party):
     _expand_case(hip, rng, vt, n0, levels, party)
 
 
+# The specialised full-domain leaves (dpf_hip_expand dispatch): uniform direct
+# tuples as FastIntLeaf lanes, mixed-width direct tuples (incl. XorWrapper
+# lanes) as SwarLeaf, tuples of IntModN32 as Mod32Leaf (Moller-Granlund
+# sampling from 1 or 2 blocks, blocks_needed >= the blocks read) -- at a size
+# where every lane runs whole subtrees, both parties.
+SPECIALISED_TYPES = [
+    ("tuple", [("int", 32), ("int", 32)]),
+    ("tuple", [("int", 16), ("int", 16), ("int", 16)]),
+    ("tuple", [("int", 32), ("int", 64)]),
+    ("tuple", [("int", 8), ("int", 16), ("int", 32), ("int", 64)]),
+    ("tuple", [("xor", 32), ("int", 32)]),
+    ("tuple", [("int", 8), ("xor", 8)]),
+    ("tuple", [("int", 64), ("xor", 64)]),
+    ("intmodn", 32, M32),
+    ("tuple", [("intmodn", 32, M32), ("intmodn", 32, M32)]),
+    ("tuple", [("intmodn", 32, 3), ("intmodn", 32, 4294967295), ("intmodn", 32, 65537)]),
+    ("tuple", [("intmodn", 32, M32)] * 4),
+]
+
+
+@pytest.mark.parametrize("vt", SPECIALISED_TYPES, ids=str)
+@pytest.mark.parametrize("party", [0, 1])
+@pytest.mark.parametrize("sec", [40.0, 96.0])
+def test_expand_specialised_leaves(hip, vt, party, sec):
+    rng = np.random.default_rng(hash((str(vt), party, sec)) & 0xFFFFFFFF)
+    _expand_case(hip, rng, vt, 3, 17, party, sec=sec)
+
+
+# The opt-in hybrid kernel (DPF_EXPAND_HYBRID=1), shapes above its threshold (>= 8 leaves per lane of a full
+# launch, dpf_expand_hybrid.hip): the leaf value hashes run bitsliced on the
+# VALU, the inner nodes on the T-table; (3, 2^18) is octets only (S = 3).
+@pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
+@pytest.mark.parametrize("levels,n0", [(21, 1), (18, 9), (3, 1 << 18)])
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_hybrid_shapes(hip, vt, levels, n0, party, monkeypatch):
+    if (levels, n0) != (21, 1) and vt not in (("int", 64), ("xor", 128), ("int", 8)):
+        pytest.skip("shape covered by the other types")
+    monkeypatch.setenv("DPF_EXPAND_HYBRID", "1")   # opt-in kernel
+    rng = np.random.default_rng(hash((str(vt), levels, n0, party, "hyb")) & 0xFFFFFFFF)
+    _expand_case(hip, rng, vt, n0, levels, party)
+
+
 @pytest.mark.parametrize("vt,cepb", [(("int", 8), 1), (("int", 8), 4), (("int", 16), 2),
                                      (("int", 32), 1), (("int", 64), 1)], ids=str)
 def test_expand_partial_blocks(hip, vt, cepb):

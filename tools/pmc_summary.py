@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Summarises one rocprofv3 collection directory (trace/ with --kernel-trace
+--stats, and p*/ PMC passes, as written by profiles/profile.sh or
+tools/hyb_profile.sh) for one kernel into the profiles/<tag>_summary.json
+format: per-launch counter averages, the sustained clock, LDS-pipe busy
+fraction, VALU / LDS instructions per AES block and HBM write bytes (WRITE_SIZE
+is in KiB on gfx950, MI355X_MICROARCH.md; GRBM_GUI_ACTIVE sums the 8 XCDs).
+
+  python tools/pmc_summary.py <dir> <kernel substring> --aes N --bytes B [--tag t]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+CUS = 256
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("kernel")
+    ap.add_argument("--aes", type=int, required=True, help="algorithmic AES blocks per launch")
+    ap.add_argument("--bytes", type=int, required=True, help="algorithmic bytes written per launch")
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    res = {"tag": a.tag}
+    for f in glob.glob(os.path.join(a.dir, "trace", "*kernel_stats.csv")):
+        for row in csv.DictReader(open(f)):
+            if a.kernel in row["Name"]:
+                res.update(kernel=row["Name"], calls=int(row["Calls"]), avg_ns=float(row["AverageNs"]),
+                           min_ns=float(row["MinNs"]))
+    sums, launches = defaultdict(float), defaultdict(set)
+    for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            if a.kernel in row["Kernel_Name"]:
+                c = row["Counter_Name"]
+                sums[c] += float(row["Counter_Value"])
+                launches[c].add(row["Dispatch_Id"])
+    per = {c: sums[c] / len(launches[c]) for c in sums}
+    res["counters_per_launch"] = per
+    aes = a.aes
+    res["aes_blocks_per_launch"] = aes
+    if "avg_ns" in res:
+        res["gaes_per_s"] = aes / res["avg_ns"]
+    if "GRBM_GUI_ACTIVE" in per and "avg_ns" in res:
+        cyc = per["GRBM_GUI_ACTIVE"] / 8
+        res["effective_clock_ghz"] = cyc / res["avg_ns"]
+        res["clk_per_aes_per_cu"] = cyc * CUS / aes
+        if "SQ_INSTS_LDS" in per:
+            res["lds_pipe_busy"] = per["SQ_INSTS_LDS"] * 2 / CUS / cyc
+    if "SQ_INSTS_VALU" in per:
+        res["valu_lane_ops_per_aes"] = per["SQ_INSTS_VALU"] * 64 / aes
+    if "SQ_INSTS_LDS" in per:
+        res["lds_lane_ops_per_aes"] = per["SQ_INSTS_LDS"] * 64 / aes
+    if "WRITE_SIZE" in per:
+        res["hbm_write_bytes"] = per["WRITE_SIZE"] * 1024
+        res["algorithmic_write_bytes"] = a.bytes
+        res["write_amplification"] = res["hbm_write_bytes"] / a.bytes
+    if "FETCH_SIZE" in per:
+        res["hbm_read_bytes_corrected"] = per["FETCH_SIZE"] * 1024 * 2
+    if "hbm_write_bytes" in res:
+        res["hbm_traffic_bytes"] = res["hbm_write_bytes"] + res.get("hbm_read_bytes_corrected", 0)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
