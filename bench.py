@@ -108,10 +108,19 @@ def _int_of(v) -> int:
     return int(v.integer.value_uint64)
 
 
-CPU_THREADS = min(16, os.cpu_count() or 1)   # the GPU box's CPU share is 16 per GPU
+def baseline_threads() -> int:
+    """Host threads for the CPU baselines: the cores this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS -- the GPU box exports the
+    per-GPU CPU share there (16) and its rules cap worker pools at that share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(cap))) if cap and cap.isdigit() else n
 
 
-def host_cpu() -> dict:
+CPU_THREADS = baseline_threads()   # 16 on the GPU box (its per-GPU CPU share)
+
+
+def host_cpu(threads: int = None) -> dict:
     """CPU model and logical CPU count of the host the baseline ran on."""
     model = None
     try:
@@ -121,7 +130,10 @@ def host_cpu() -> dict:
                 break
     except OSError:
         pass
-    return {"model": model, "nproc": os.cpu_count(), "threads_used": CPU_THREADS}
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "threads_used": threads if threads is not None else CPU_THREADS}
 
 
 def run_cpu_pool(work, items, threads: int = CPU_THREADS, budget_s: float = 15.0):
@@ -305,6 +317,8 @@ def main():
         vtype, beta_py = D.integer_type(bits), 0xDEADBEEF
     params.value_type.CopyFrom(vtype)
     dpf = D.DistributedPointFunction.create(params)
+    if args.workload == "full_domain_tuple":
+        dpf.register_value_type(vtype)
     # Same key on every rank: root seeds injected (GenerateKeysIncrementalWithSeeds).
     alpha = 0x2545F4914F6CDD1D % (1 << log_domain)
     beta = D.to_value(vtype, beta_py)
@@ -424,23 +438,48 @@ def _oracle_key(key):
             "last_vc": [[_int_of(v)] for v in key.last_level_value_correction]}
 
 
-def cpu_baseline_points(dpf, batch, points_fn, keys: int, ppk: int):
-    """The oracle's EvaluateAtImpl (C restatement of distributed_point_function.h:
-    839-1010 over OpenSSL AES-NI in 64-block batches) on CPU_THREADS host threads,
-    on a bounded sample of the workload: keys of the batch x ppk points, 15 s."""
+def cpu_baseline_points(dpf, batch, host_points, keys: int, ppk: int):
+    """The reference's EvaluateAt CPU path (EvaluateAtImpl, distributed_point_
+    function.h:839-1010, with the Highway one-AES-per-level EvaluateSeeds,
+    evaluate_prg_hwy.cc:205-304) restated on AES-NI (oracle/cpu_baseline.c, 8
+    points interleaved per thread; tests/test_oracle.py checks it equals the
+    oracle) on a bounded sample of the workload: the first keys of the batch x
+    their ppk points, chunks of 32 keys spread over baseline_threads() host
+    threads for ~15 s, plus a 3 s single-thread sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    P = O.OracleParams([(128, ("int", 64), 0)])
+    nk = min(keys, 32768)
+    protos = [dpf.key_from_batch(batch, k) for k in range(nk)]
+    L = len(protos[0].correction_words) - 1          # 127 tree levels below the root
+    seeds = np.array([[p.seed.low, p.seed.high] for p in protos], np.uint64)
+    party = np.array([p.party for p in protos], np.uint8)
+    cws = np.array([[[c.seed.low, c.seed.high] for c in p.correction_words[:L]] for p in protos],
+                   np.uint64)
+    cl = np.array([[c.control_left for c in p.correction_words[:L]] for p in protos], np.uint8)
+    cr = np.array([[c.control_right for c in p.correction_words[:L]] for p in protos], np.uint8)
+    vcw = np.array([[[_int_of(v) & (2**64 - 1), 0] for v in p.last_level_value_correction]
+                    for p in protos], np.uint64)
+    pts = np.ascontiguousarray(host_points[:nk * ppk].reshape(nk, ppk, 2))
+    chunk = 32
 
-    def work(k):
-        okey = _oracle_key(dpf.key_from_batch(batch, k))
-        return O.evaluate_at(P, okey, 0, points_fn(k)).shape[0]
+    def work(c):
+        sl = slice(c * chunk, min(nk, (c + 1) * chunk))
+        O.baseline_evaluate_at_u64(L, 1, seeds[sl], party[sl], cws[sl], cl[sl], cr[sl], vcw[sl],
+                                   pts[sl])
+        return (sl.stop - sl.start) * ppk
 
-    n, dt, done = run_cpu_pool(work, range(keys), budget_s=15.0)
-    return {"value": n / dt, "unit": "points/s", "cores": CPU_THREADS, "kind": "port", "host": host_cpu(),
-            "sample": f"{done} keys x {ppk} points of the benchmark batch (log 128, uint64): "
-                      f"EvaluateSeeds over 127 levels + value hash + correction (oracle over "
-                      f"OpenSSL AES-NI); {dt:.1f} s wall on {CPU_THREADS} host threads",
+    T = baseline_threads()
+    n, dt, done = run_cpu_pool(work, range((nk + chunk - 1) // chunk), threads=T, budget_s=15.0)
+    n1, dt1, done1 = run_cpu_pool(work, range((nk + chunk - 1) // chunk), threads=1, budget_s=3.0)
+    return {"value": n / dt, "unit": "points/s", "cores": T, "kind": "port", "host": host_cpu(T),
+            "single_thread_value": n1 / dt1,
+            "published_reference_single_thread": "335K points/s (2^20 points at log 128 in "
+                                                 "3.13 s, experiments/README.md:98-107, one "
+                                                 "Xeon thread @ 2.3 GHz)",
+            "sample": f"{done * chunk} keys x {ppk} points of the benchmark batch (log 128, "
+                      f"uint64): the reference's one-AES-per-level path walk + value hash + "
+                      f"correction on AES-NI (oracle/cpu_baseline.c); {dt:.1f} s wall on {T} "
+                      f"host threads",
             "aes_blocks_per_s": n * 128 / dt}
 
 
@@ -591,14 +630,12 @@ def main_evaluate_at(args):
             "process_group": ginfo,
         }
         if world == 1 and not args.no_cpu_baseline:
-            host_pts = None if summed else points.view(-1, 2)
-
-            def pts_of(k):
-                if summed:
-                    return [int(a) | int(b) << 64 for a, b in shared.tolist()]
-                pk = host_pts[k * ppk:(k + 1) * ppk].cpu().numpy().view(np.uint64)
-                return [int(a) | int(b) << 64 for a, b in pk.tolist()]
-            res["cpu_baseline"] = cpu_baseline_points(dpf, b0, pts_of, nk, ppk)
+            nb = min(nk, 32768)
+            if summed:
+                host_pts = np.tile(shared.astype(np.uint64), (nb, 1))
+            else:
+                host_pts = points.view(-1, 2)[:nb * ppk].cpu().numpy().view(np.uint64)
+            res["cpu_baseline"] = cpu_baseline_points(dpf, b0, host_pts, nk, ppk)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -129,7 +129,7 @@ def build_host(force=False):
 def build_oracle(force=False):
     odir = os.path.join(ROOT, "oracle")
     out = os.path.join(odir, "liboracle_dpf.so")
-    if force or _stale(out, [os.path.join(odir, "dpf_oracle.c")]):
+    if force or _stale(out, [os.path.join(odir, "dpf_oracle.c"), os.path.join(odir, "cpu_baseline.c")]):
         _run(["make", "-C", odir, "-B" if force else "liboracle_dpf.so"])
     return out
 

@@ -137,7 +137,12 @@ done:
 }
 
 /* ------------------------------------------------------------------------- */
-/* a9: EvaluateSeeds, scalar semantics (dpf/internal/evaluate_prg_hwy.cc:415-491) */
+/* a9: EvaluateSeeds (dpf/internal/evaluate_prg_hwy.cc:415-491).  The scalar    */
+/* fallback hashes both children and keeps one; the Highway kernel             */
+/* (:205-304) hashes each seed once, with the key its path bit selects.  The   */
+/* outputs are the same; this restatement does the latter (seeds grouped by    */
+/* path bit, one EVP batch per key), so the oracle-based CPU baselines run the */
+/* reference's one-AES-per-level work.                                         */
 /* ------------------------------------------------------------------------- */
 
 int oracle_evaluate_seeds(const uint8_t key_left[16], const uint8_t key_right[16],
@@ -155,19 +160,24 @@ int oracle_evaluate_seeds(const uint8_t key_left[16], const uint8_t key_right[16
   if (!st) st = prg_init(&pr, key_right);
   if (st) return st;
   u128 bl[ORACLE_BATCH], br[ORACLE_BATCH];
+  int64_t il[ORACLE_BATCH], ir[ORACLE_BATCH];
   uint8_t pb[ORACLE_BATCH], cb[ORACLE_BATCH];
   for (int64_t start = 0; start < n; start += ORACLE_BATCH) {
     int64_t bs = n - start < ORACLE_BATCH ? n - start : ORACLE_BATCH;
     for (int level = 0; level < L; ++level) {
       const u128* src = (level == 0 ? seeds_in : seeds_out) + start;
-      if ((st = prg_eval(&pl, src, bl, bs))) goto done;
-      if ((st = prg_eval(&pr, src, br, bs))) goto done;
       int bit_index = L - level - 1; /* evaluate_prg_hwy.cc:452 */
+      int64_t nl = 0, nr = 0;
       for (int64_t i = 0; i < bs; ++i) {
         pb[i] = 0;
         if (bit_index < 128) pb[i] = (uint8_t)((paths[start + i] >> bit_index) & 1);
-        seeds_out[start + i] = pb[i] ? br[i] : bl[i];
+        if (pb[i]) { br[nr] = src[i]; ir[nr++] = i; }
+        else { bl[nl] = src[i]; il[nl++] = i; }
       }
+      if (nl && (st = prg_eval(&pl, bl, bl, nl))) goto done;
+      if (nr && (st = prg_eval(&pr, br, br, nr))) goto done;
+      for (int64_t j = 0; j < nl; ++j) seeds_out[start + il[j]] = bl[j];
+      for (int64_t j = 0; j < nr; ++j) seeds_out[start + ir[j]] = br[j];
       memcpy(cb, (level == 0 ? ctrl_in : ctrl_out) + start, bs);
       for (int64_t i = 0; i < bs; ++i) { /* :470-486 */
         uint8_t t = cb[i] & 1;

@@ -99,6 +99,9 @@ def lib():
         L.oracle_packed_element_size.argtypes = [P]
         U = ctypes.c_uint64
         L.oracle_generate_keys.argtypes = [P, P, P, P, P, U, U, P, U, U, U, U, P, P, P, P]
+        I64 = ctypes.c_int64
+        L.baseline_evaluate_at_u64.argtypes = [P, P, P, I64, I64, ctypes.c_int, ctypes.c_int, P, P,
+                                               P, P, P, I64, P, P, P]
         _LIB = L
     return _LIB
 
@@ -121,6 +124,25 @@ def blocks_from_ints(xs: Sequence[int]) -> np.ndarray:
 
 def ints_from_blocks(a: np.ndarray) -> List[int]:
     return [int(lo) | (int(hi) << 64) for lo, hi in a]
+
+
+def baseline_evaluate_at_u64(L: int, bib: int, key_seed: np.ndarray, party: np.ndarray,
+                             cw_seed: np.ndarray, cw_left: np.ndarray, cw_right: np.ndarray,
+                             vcw: np.ndarray, points: np.ndarray) -> np.ndarray:
+    """bench.py's CPU baseline for batched EvaluateAt<uint64_t> (cpu_baseline.c:
+    the reference's one-AES-per-level path walk on AES-NI, 8 points
+    interleaved).  key_seed (K, 2) u64 blocks, party (K,) u8, cw_* (K, L) rows,
+    vcw (K, 2, 2) u64 blocks (two elements), points (K, P, 2) u64 blocks.
+    Releases the GIL (ctypes), so host threads run it in parallel."""
+    K, Pn = points.shape[0], points.shape[1]
+    out = np.empty((K, Pn), np.uint64)
+    args = [np.ascontiguousarray(a) for a in (key_seed, party, cw_seed, cw_left, cw_right, vcw,
+                                               points)]
+    lib().baseline_evaluate_at_u64(key_bytes(PRG_KEY_LEFT), key_bytes(PRG_KEY_RIGHT),
+                                   key_bytes(PRG_KEY_VALUE), K, Pn, L, bib,
+                                   *[_ptr(a) for a in args[:5]], cw_seed.shape[1],
+                                   _ptr(args[5]), _ptr(args[6]), _ptr(out))
+    return out
 
 
 # --------------------------------------------------------------------------

@@ -8,7 +8,11 @@ outputs in a test's time):
   two-party property at full size), and sampled 2^12-output windows are
   bit-exact against the oracle's ExpandSeeds + HashExpandedSeeds;
 * config 4: 2^20 keys x 2^10 shared points, summed over keys on the device for
-  both parties: the shares reconstruct the number of keys hitting each point.
+  both parties: the shares reconstruct the number of keys hitting each point;
+  and per key (2^30 outputs): planted hits reconstruct to beta, every other
+  output to 0, four keys' rows bit-exact against the oracle;
+* config 5b: one full heavy-hitters pass (2^20 clients, 61 levels, both
+  servers) reconstructs the plaintext prefix histogram at every level.
 """
 import numpy as np
 import pytest
@@ -126,3 +130,70 @@ def test_config4_batched_points_reconstruct_hit_counts():
         sums.append(out.cpu().numpy().view(np.uint64).astype(object))
     rec = [(int(x) + int(y)) % (1 << 64) for x, y in zip(*sums)]
     assert rec == [3 * int(h) for h in hits]
+
+
+def test_config4_per_key_outputs_full_size():
+    """Config 4 at full size, per-key outputs (EvaluateAtBatchToDevice): 2^20
+    keys x 2^10 independent points each on the 2^128 domain.  Every key's
+    alpha is planted at point slot k % 1024, so the two parties' 2^30 outputs
+    add up to beta at exactly those 2^20 slots and to 0 at every other slot;
+    four keys' 1024-point rows are bit-exact against the oracle's EvaluateAt."""
+    import torch
+    dpf = D.DistributedPointFunction.create(_params(128, 64))
+    n_keys, ppk = 1 << 20, 1 << 10
+    rng = np.random.default_rng(4444)
+    alphas = rng.integers(0, 2**64, size=(n_keys, 2), dtype=np.uint64)
+    seeds = rng.integers(0, 2**64, size=(2 * n_keys, 2), dtype=np.uint64)
+    beta = 0x0123_4567_89AB_CDEF
+    b0, b1 = dpf.generate_key_batch(alphas, [D.to_value(D.integer_type(64), beta)],
+                                    root_seeds=seeds, threads=16)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4444)
+    pts = torch.randint(-2**63, 2**63 - 1, (n_keys * ppk, 2), dtype=torch.int64, device="cuda",
+                        generator=g)
+    keys_idx = torch.arange(n_keys, device="cuda")
+    slot = keys_idx * ppk + (keys_idx % ppk)
+    pts[slot] = torch.from_numpy(alphas.view(np.int64)).cuda()
+    outs = []
+    for b in (b0, b1):
+        out = torch.empty(n_keys * ppk, dtype=torch.int64, device="cuda")
+        dpf.evaluate_at_batch_to_device(dpf.upload_key_batch(b), 0, pts, ppk, out)
+        outs.append(out)
+    torch.cuda.synchronize()
+    s = outs[0] + outs[1]                  # mod 2^64 in int64
+    assert int((s != 0).sum()) == n_keys
+    assert bool((s[slot] == beta).all())
+    host_pts = pts.view(n_keys, ppk, 2)
+    for k in (0, 1, 123457, n_keys - 1):
+        okey = _oracle_key(dpf.key_from_batch(b0, k))
+        row = host_pts[k].cpu().numpy().view(np.uint64)
+        want = O.evaluate_at(O.OracleParams([(128, ("int", 64), 0)]), okey, 0,
+                             [int(a) | int(h) << 64 for a, h in row])
+        got = outs[0][k * ppk:(k + 1) * ppk].cpu().numpy().view(np.uint8).reshape(ppk, 8)
+        np.testing.assert_array_equal(got, want, err_msg=f"key {k}")
+
+
+def test_config5b_heavy_hitters_full_size():
+    """Config 5b at full size: 2^20 clients, the 61-level 128-bit hierarchy,
+    Tuple<IntModN32 x 2>, top-1024 candidates per level, both servers, one
+    full pass; at every level the two servers' key sums reconstruct the
+    plaintext prefix histogram exactly (HH.verify)."""
+    import torch
+    from distributed_point_functions_amd import heavy_hitters as HH
+    logs = HH.hierarchy()
+    dpf = HH.create_dpf(logs)
+    n_keys, top_k = 1 << 20, 1024
+    values, idx, alphas = HH.client_values(n_keys, seed=0x5B)
+    seeds = np.random.default_rng(0x5B5B).integers(0, 2**64, size=(2 * n_keys, 2), dtype=np.uint64)
+    beta = D.to_value(HH.value_type(), HH.BETA)
+    b0, b1 = dpf.generate_key_batch(alphas, [beta] * len(logs), root_seeds=seeds, threads=16)
+    max_out = max(4 * top_k, 1 << logs[0])
+    servers = [HH.Server(dpf, dpf.upload_key_batch(b), max_out, torch.device("cuda"))
+               for b in (b0, b1)]
+    rec = []
+    final = HH.run(dpf, servers, logs, top_k=top_k, record=rec)
+    assert len(rec) == len(logs) == 61
+    HH.verify(rec, logs, values, idx)
+    ref = HH.plaintext_prefix_counts(values, idx, 128)
+    head = sorted(ref, key=lambda v: (-ref[v], v))[:8]
+    assert set(head) <= set(final)
