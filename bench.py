@@ -210,23 +210,27 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
             "aes_blocks_per_s": done * (tree_aes_per_launch(sub) + top) / dt}
 
 
-def profiled_traffic(leaves_per_launch: int):
+def profiled_traffic(kernel: str, leaves_per_launch: int = None):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
-    rocprofv3 PMC summary for this workload (profiles/<round>_summary.json,
-    FETCH_SIZE/WRITE_SIZE with the gfx950 corrections of MI355X_MICROARCH.md)."""
+    rocprofv3 PMC summary whose kernel name contains `kernel` (and, for the
+    full domain, the same outputs per launch): profiles/<round>_summary.json,
+    written by tools/pmc_summary.py from profiles/profile.sh's passes
+    (FETCH_SIZE/WRITE_SIZE with the gfx950 corrections of MI355X_MICROARCH.md)."""
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
         try:
             s = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if (s.get("leaves_per_launch") == leaves_per_launch and "hbm_traffic_bytes" in s
-                and "expand_kernel" in s.get("kernel", "")):
+        if ("hbm_traffic_bytes" in s and kernel in s.get("kernel", "")
+                and (leaves_per_launch is None or s.get("leaves_per_launch") == leaves_per_launch)):
             best = (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT),
                     {"valu_lane_ops_per_aes": s.get("valu_lane_ops_per_aes"),
                      "lds_lane_ops_per_aes": s.get("lds_lane_ops_per_aes"),
+                     "lds_pipe_busy": s.get("lds_pipe_busy"),
                      "sustained_clock_ghz": s.get("effective_clock_ghz"),
                      "clk_per_aes_per_cu": s.get("clk_per_aes_per_cu"),
+                     "write_amplification": s.get("write_amplification"),
                      "profiled_launch_ms": s.get("avg_ns", 0) / 1e6})
     return best
 
@@ -375,7 +379,8 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = profiled_traffic(outputs_per_rank) if args.workload == "full_domain" else None
+        tr = (profiled_traffic("expand_kernel<(anonymous namespace)::FastIntLeaf<64, false>",
+                               outputs_per_rank) if args.workload == "full_domain" else None)
         vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
                  "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "
                                                       "IntModN<uint32_t, 4294967291>>",
@@ -607,6 +612,9 @@ def main_evaluate_at(args):
     depth = dpf.hierarchy_to_tree()[0]                 # 127 path levels, + 1 value hash
     aes_per_launch = nk * ppk * (depth + 1)
     achieved = aes_per_launch / (kern_ms_max * 1e-3) / 1e9
+    kname = ("eval_points_kernel<(anonymous namespace)::GenericLeaf, 64, true, true, %s" %
+             ("true>" if summed else "false, true>"))
+    tr = profiled_traffic(kname) if n_keys == 1 << 20 and world == 1 else None
     if rank == 0:
         res = {
             "metric": EA_SUM_METRIC if summed else EA_METRIC,
@@ -624,8 +632,8 @@ def main_evaluate_at(args):
                        "parallelism": f"key-batch x{world}"},
             "aes_blocks_per_s": n_keys * ppk * (depth + 1) * args.steps / elapsed,
             "keygen_s_rank0": keygen_s, "keygen_threads": threads, "key_ingest_rank0": ingest,
-            **aes_rooflines(achieved, "eval_points_kernel<GenericLeaf, 64, true, true, %s>" %
-                            ("true" if summed else "false"), traffic=None,
+            **aes_rooflines(achieved, kname, traffic=tr[0] if tr else None,
+                            traffic_source=tr[1] if tr else None, pmc=tr[2] if tr else None,
                             launch_ms=kern_ms_max, algorithmic_aes_per_launch=aes_per_launch),
             "process_group": ginfo,
         }
@@ -786,6 +794,8 @@ def main_heavy_hitters(args):
     aes_rank = HH.algorithmic_aes(dpf, logs, record, hi - lo) * 2
     aes_total = HH.algorithmic_aes(dpf, logs, record, n_keys) * 2
     achieved = aes_rank / (kern_ms_max * 1e-3) / 1e9
+    tr = (profiled_traffic("batch_level_kernel<(anonymous namespace)::Mod32V<2, true>, 2, true>")
+          if n_keys == 1 << 20 and world == 1 and args.top_k == 1024 else None)
     if rank == 0:
         ref = HH.plaintext_prefix_counts(values, idx, 128)
         true_top = set(sorted(ref, key=lambda v: (-ref[v], v))[:args.top_k])
@@ -809,7 +819,9 @@ def main_heavy_hitters(args):
             "keygen_s_rank0": keygen_s, "keygen_threads": threads,
             "verified": "two-server reconstruction == plaintext prefix histogram at every level",
             "true_top_k_recall": len(true_top & set(final)) / max(len(true_top), 1),
-            **aes_rooflines(achieved, "batch_level_kernel<Mod32V, 2, true>", traffic=None,
+            **aes_rooflines(achieved, "batch_level_kernel<Mod32V, 2, true>",
+                            traffic=tr[0] if tr else None, traffic_unit="bytes per pass",
+                            traffic_source=tr[1] if tr else None, pmc=tr[2] if tr else None,
                             launch_ms_per_pass=kern_ms_max, algorithmic_aes_per_pass=aes_rank),
             "process_group": ginfo,
         }
@@ -903,6 +915,8 @@ def main_dcf(args):
     aes_per_eval = h2t[-1] + (h2t[-1] + 1)      # walk + one value hash per depth
     aes_launch = nk * ppk * aes_per_eval
     achieved = aes_launch / (kern_ms_max * 1e-3) / 1e9
+    tr = (profiled_traffic("dcf_eval_kernel<64, true>")
+          if (n_keys, ppk, n, world) == (1 << 16, 1 << 10, 64, 1) else None)
     if rank == 0:
         res = {
             "metric": DCF_METRIC, "value": n_keys * ppk * args.steps / elapsed, "unit": "evals/s",
@@ -916,7 +930,8 @@ def main_dcf(args):
                        "log_domain_size": n, "parallelism": f"key-batch x{world}"},
             "aes_blocks_per_s": n_keys * ppk * aes_per_eval * args.steps / elapsed,
             "keygen_s_rank0": keygen_s,
-            **aes_rooflines(achieved, "dcf_eval_kernel<64, true>", traffic=None,
+            **aes_rooflines(achieved, "dcf_eval_kernel<64, true>", traffic=tr[0] if tr else None,
+                            traffic_source=tr[1] if tr else None, pmc=tr[2] if tr else None,
                             launch_ms=kern_ms_max, algorithmic_aes_per_launch=aes_launch),
             "process_group": ginfo,
         }

@@ -25,24 +25,39 @@ def main():
     ap.add_argument("--aes", type=int, required=True, help="algorithmic AES blocks per launch")
     ap.add_argument("--bytes", type=int, required=True, help="algorithmic bytes written per launch")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--total", action="store_true",
+                    help="sum every matching dispatch (a workload of many differently sized "
+                         "launches, e.g. one heavy-hitters pass): --aes/--bytes are totals")
+    ap.add_argument("--leaves", type=int, default=None,
+                    help="outputs per launch (full domain; bench.py's profiled_traffic key)")
     a = ap.parse_args()
     res = {"tag": a.tag}
-    for f in glob.glob(os.path.join(a.dir, "trace", "*kernel_stats.csv")):
+    # Per-launch mode keeps only the launches with the largest grid: a bench
+    # run's spot checks call the same kernel on a few points.
+    durs = []
+    for f in glob.glob(os.path.join(a.dir, "trace", "*kernel_trace.csv")):
         for row in csv.DictReader(open(f)):
-            if a.kernel in row["Name"]:
-                res.update(kernel=row["Name"], calls=int(row["Calls"]), avg_ns=float(row["AverageNs"]),
-                           min_ns=float(row["MinNs"]))
+            if a.kernel in row["Kernel_Name"]:
+                durs.append((int(row["Grid_Size_X"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"]),
+                             row["Kernel_Name"]))
+    grid = max(g for g, _, _ in durs) if durs else None
+    if durs:
+        sel = [d for g, d, _ in durs if a.total or g == grid]
+        res.update(kernel=durs[0][2], calls=len(sel),
+                   avg_ns=(sum(sel) if a.total else sum(sel) / len(sel)), min_ns=min(sel))
     sums, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            if a.kernel in row["Kernel_Name"]:
+            if a.kernel in row["Kernel_Name"] and (a.total or int(row["Grid_Size"]) == grid):
                 c = row["Counter_Name"]
                 sums[c] += float(row["Counter_Value"])
                 launches[c].add(row["Dispatch_Id"])
-    per = {c: sums[c] / len(launches[c]) for c in sums}
+    per = {c: sums[c] / (1 if a.total else len(launches[c])) for c in sums}
     res["counters_per_launch"] = per
     aes = a.aes
     res["aes_blocks_per_launch"] = aes
+    if a.leaves:
+        res["leaves_per_launch"] = a.leaves
     if "avg_ns" in res:
         res["gaes_per_s"] = aes / res["avg_ns"]
     if "GRBM_GUI_ACTIVE" in per and "avg_ns" in res:
@@ -57,8 +72,9 @@ def main():
         res["lds_lane_ops_per_aes"] = per["SQ_INSTS_LDS"] * 64 / aes
     if "WRITE_SIZE" in per:
         res["hbm_write_bytes"] = per["WRITE_SIZE"] * 1024
-        res["algorithmic_write_bytes"] = a.bytes
-        res["write_amplification"] = res["hbm_write_bytes"] / a.bytes
+        if a.bytes > 0:
+            res["algorithmic_write_bytes"] = a.bytes
+            res["write_amplification"] = res["hbm_write_bytes"] / a.bytes
     if "FETCH_SIZE" in per:
         res["hbm_read_bytes_corrected"] = per["FETCH_SIZE"] * 1024 * 2
     if "hbm_write_bytes" in res:
