@@ -112,6 +112,13 @@ struct ValueTypeHelper<T, std::enable_if_t<is_unsigned_integer<T>::value>> {
   }
   static void ToLeaves(const T& v, uint128* out) { out[0] = static_cast<uint128>(v); }
   static T FromLeaves(const uint128* in) { return static_cast<T>(in[0]); }
+  // Packed element image (little-endian, leaves back to back): sizeof(T) bytes.
+  static constexpr int kPackedBytes = sizeof(T);
+  static T FromPacked(const uint8_t* p) {
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    return v;
+  }
 };
 
 // IntModN.
@@ -133,6 +140,12 @@ struct ValueTypeHelper<IntModNImpl<B, M, kModulus>, void> {
   }
   static void ToLeaves(const Type& v, uint128* out) { out[0] = static_cast<uint128>(v.value()); }
   static Type FromLeaves(const uint128* in) { return Type(static_cast<B>(in[0])); }
+  static constexpr int kPackedBytes = sizeof(B);
+  static Type FromPacked(const uint8_t* p) {
+    B v;
+    std::memcpy(&v, p, sizeof(B));
+    return Type(v);
+  }
 };
 
 // XorWrapper.
@@ -155,6 +168,12 @@ struct ValueTypeHelper<XorWrapper<T>, void> {
   }
   static XorWrapper<T> FromLeaves(const uint128* in) {
     return XorWrapper<T>(static_cast<T>(in[0]));
+  }
+  static constexpr int kPackedBytes = sizeof(T);
+  static XorWrapper<T> FromPacked(const uint8_t* p) {
+    T v;
+    std::memcpy(&v, p, sizeof(T));
+    return XorWrapper<T>(v);
   }
 };
 
@@ -188,8 +207,19 @@ struct ValueTypeHelper<Tuple<E...>, void> {
     // Braced init list: left-to-right evaluation.
     return Type(typename Type::Base{Take<E>(in, pos)...});
   }
+  static constexpr int kPackedBytes = (ValueTypeHelper<E>::kPackedBytes + ... + 0);
+  static Type FromPacked(const uint8_t* p) {
+    int off = 0;
+    return Type(typename Type::Base{TakePacked<E>(p, off)...});
+  }
 
  private:
+  template <typename X>
+  static X TakePacked(const uint8_t* p, int& off) {
+    X x = ValueTypeHelper<X>::FromPacked(p + off);
+    off += ValueTypeHelper<X>::kPackedBytes;
+    return x;
+  }
   template <typename X>
   static X Take(const uint128* in, int& pos) {
     X x = ValueTypeHelper<X>::FromLeaves(in + pos);
@@ -245,6 +275,15 @@ std::vector<T> UnpackElements(const FlatValueType& flat, const uint8_t* data, in
     }
   }
   std::vector<T> out = MakeOutputVector<T>(n);
+  if (flat.packed_size == ValueTypeHelper<T>::kPackedBytes) {
+    // The packed layout of T is known at compile time: fixed-width loads of
+    // each leaf straight into the element (no per-leaf uint128 round trip).
+    const int step = flat.packed_size;
+    ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i) out[i] = ValueTypeHelper<T>::FromPacked(data + i * step);
+    });
+    return out;
+  }
   ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
     std::vector<uint128> leaves(flat.leaves.size());
     for (int64_t i = lo; i < hi; ++i) {
