@@ -51,7 +51,7 @@ AES_VALU_PEAK_GBLOCKS = 245.8
 AES_LDS_PEAK_GBLOCKS = 122.9
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
 METRIC = "DPF leaf evals/sec, full-domain 2^30 uint64 at 1/2/4/8 GPUs; AES blocks/s"
-KERNEL = "expand_kernel<FastIntLeaf<64, false> >"
+KERNEL = "expand_octet_kernel<64, false>"
 
 
 def parse():
@@ -238,7 +238,7 @@ def profiled_traffic(kernel: str, leaves_per_launch: int = None):
 def kernel_name(args, bits: int) -> str:
     if args.workload == "full_domain_tuple":
         return ("expand_kernel<Mod32Leaf<2> >" if args.tuple_type == "intmodn32x2"
-                else "expand_kernel<FastIntLeaf<32, false> >")
+                else "expand_octet_kernel<32, false>")
     return KERNEL.replace("64", str(bits))
 
 
@@ -379,8 +379,8 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = (profiled_traffic("expand_kernel<(anonymous namespace)::FastIntLeaf<64, false>",
-                               outputs_per_rank) if args.workload == "full_domain" else None)
+        tr = (profiled_traffic("expand_octet_kernel<64, false>", outputs_per_rank)
+              if args.workload == "full_domain" else None)
         vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
                  "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "
                                                       "IntModN<uint32_t, 4294967291>>",

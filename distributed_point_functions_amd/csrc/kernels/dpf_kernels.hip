@@ -199,6 +199,96 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
   }
 }
 
+// Octet form of expand_kernel for integer leaves that fill whole 16-byte
+// blocks (uint64, uint128, XorWrapper, uniform tuples; the default for them):
+// the bottom three levels of every subtree are expanded breadth-first as an
+// octet -- the node's 2 children (ILP2), its 4 grandchildren (ILP4), then per
+// half its 4 leaf seeds and their 4 value hashes (ILP4 each) -- and each lane
+// writes its 8 corrected blocks as 2 x 64 contiguous bytes, i.e. whole
+// 128-byte lines (expand_kernel's 32-byte leaf-pair pieces measured write
+// amplification 1.25).  The DFS stack above the octets lives in scratch (one
+// 16-byte store per push, one load per octet, issued an octet ahead) so the
+// VGPRs go to the ILP4 chains (128 VGPRs plus 160 B/lane of spills remain;
+// that scratch traffic, not the outputs, is most of its HBM bytes beyond the
+// 8 GiB written).  Measured same-box at config 2: 18.58 vs 18.87-18.98 ms per
+// 2^30 outputs with identical outputs (tools/octet_check.py); in the bench
+// 17.9 ms per step (59.95 G leaves/s).
+template <int BITS, bool XOR>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
+    ExpandParams p, FastIntLeaf<BITS, XOR> leaf) {
+  __shared__ LdsImage lds;
+  leaf.init();
+  fill_tables(lds.tab);
+  fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const int k0 = p.k0, S = p.S;
+  const int G = S - 3;
+  const int64_t ngroups = (int64_t)1 << G;
+  const UniformRK rv[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
+                           UniformRK{p.rkv.k}};
+  for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
+       item += (int64_t)gridDim.x * blockDim.x) {
+    // 1. walk from the start seed to this item's subtree root.
+    const int64_t r = item >> k0;
+    Block4 s = load_block(p.seeds_in + r);
+    uint32_t t = p.ctrl_in[r] & 1u;
+    for (int j = 0; j < k0; ++j) {
+      const uint32_t bit = (uint32_t)((item >> (k0 - 1 - j)) & 1);
+      path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
+    }
+    // 2. depth-first down to the octet roots; right children parked in
+    //    sib[d] (scratch), their control bits in tb.
+    Block4 sib[kGMax];
+    uint32_t tb = 0;
+    const int64_t leaf_base = item << S;
+    Block4 next = s;
+    for (int64_t g = 0; g < ngroups; ++g) {
+      Block4 node = next;
+      uint32_t nt = t;
+      int ds = 0;
+      if (g != 0) {
+        ds = G - (int)__builtin_ctzll((unsigned long long)g);
+        nt = (tb >> ds) & 1u;
+      }
+      for (int d = ds; d < G; ++d) {
+        Block4 c0, c1;
+        uint32_t t0, t1;
+        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d],
+                      c0, t0, c1, t1);
+        sib[d] = c1;
+        tb = (tb & ~(1u << (d + 1))) | (t1 << (d + 1));
+        node = c0;
+        nt = t0;
+      }
+      // The next octet's root (written by now), loaded an octet ahead.
+      if (g + 1 < ngroups) next = sib[G - (int)__builtin_ctzll((unsigned long long)(g + 1)) - 1];
+      // 3. the octet.
+      const int lvl = k0 + G;
+      Block4 c[2], q[4];
+      uint32_t ct[2], qt[4];
+      children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c[0],
+                    ct[0], c[1], ct[1]);
+      children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
+                       lds.cw_ctrl[lvl + 1], q, qt);
+      uint4* o = reinterpret_cast<uint4*>(p.out + (leaf_base + 8 * g) * 16);
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        Block4 l[4];
+        uint32_t lt[4];
+        children_step_x2(lk, p.rkl.k, p.rkr.k, q[2 * hf], qt[2 * hf], q[2 * hf + 1],
+                         qt[2 * hf + 1], lds.cw_seed[lvl + 2], lds.cw_ctrl[lvl + 2], l, lt);
+        dpf_aes::mmo_hashN<4>(l, lk, rv);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const Block4 h = leaf.correct(l[j], lt[j]);
+          o[4 * hf + j] = make_uint4(h.w0, h.w1, h.w2, h.w3);
+        }
+      }
+    }
+  }
+}
+
 // Batched point evaluation (row a11).  Work item u covers
 // key k and the point PAIR (q, q + half) of that key, hashed as two
 // interleaved chains (ILP2).  With UNIFORM, half % 64 == 0, so all 64 lanes of
@@ -476,9 +566,27 @@ int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
   return kOk;
 }
 
+// The octet kernel takes integer leaves filling whole blocks whenever the
+// subtrees have >= 8 leaves (DPF_EXPAND_NO_OCTET=1 forces expand_kernel).
+template <int BITS, bool XOR>
+bool launch_octet(const ExpandParams& p, const dpf_block* vcw, int E, int party, int store_bytes,
+                  hipStream_t s) {
+  const char* off = getenv("DPF_EXPAND_NO_OCTET");
+  if ((off && off[0] == '1') || store_bytes != 16 || p.S < 3) return false;
+  const int blk = block_for(p.num_items);
+  hipLaunchKernelGGL((expand_octet_kernel<BITS, XOR>), dim3(grid_for(p.num_items, blk)), dim3(blk),
+                     0, s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
+  return true;
+}
+
 template <int BITS>
 int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf_block* vcw,
                        int E, int party, int store_bytes, hipStream_t s) {
+  if (d->kind[0] == DPF_LEAF_XOR ? launch_octet<BITS, true>(p, vcw, E, party, store_bytes, s)
+                                 : launch_octet<BITS, false>(p, vcw, E, party, store_bytes, s)) {
+    HIP_TRY(hipGetLastError());
+    return kOk;
+  }
   if (d->kind[0] == DPF_LEAF_XOR)
     return launch_expand(p, FastIntLeaf<BITS, true>{vcw, E, party, store_bytes, {}}, s);
   return launch_expand(p, FastIntLeaf<BITS, false>{vcw, E, party, store_bytes, {}}, s);
