@@ -437,6 +437,125 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(Poin
   }
 }
 
+// Four path walks per lane (ILP4) for integer / XorWrapper leaves: item u
+// covers points (q, q + part, q + 2 part, q + 3 part) of its key (or key
+// chunk in sum mode), part = ceil(P / 4); otherwise as eval_points_kernel.
+// Opt-in (DPF_POINTS_QUAD=1) for per-key (non-sum) launches: 112-122 VGPRs
+// cost more occupancy than the extra ILP buys; a sum form would spill.
+template <int N>
+__device__ __forceinline__ void path_stepN(const LdsLookup& lk, const RoundKeys& rkl,
+                                           const RoundKeys& rkd, Block4* s, uint32_t* t,
+                                           const uint32_t* b, uint4 cs, uint32_t cctl) {
+  Block4 h[N];
+  SelectRK rk[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    h[i] = s[i];
+    rk[i] = SelectRK{rkl.k, rkd.k, 0u - b[i]};
+  }
+  dpf_aes::mmo_hashN<N>(h, lk, rk);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t m = 0u - t[i];
+    h[i].w0 ^= cs.x & m; h[i].w1 ^= cs.y & m; h[i].w2 ^= cs.z & m; h[i].w3 ^= cs.w & m;
+    const uint32_t n = (h[i].w0 & 1u) ^ (t[i] & ((cctl >> b[i]) & 1u));
+    h[i].w0 &= ~1u;
+    s[i] = h[i];
+    t[i] = n;
+  }
+}
+
+template <int BITS, bool UNIFORM, bool SUM>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(PointParams p) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const int L = p.num_levels;
+  const int64_t P = p.points_per_key, part = p.half;
+  const UniformRK rv[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
+                           UniformRK{p.rkv.k}};
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    int64_t grp = u / part;
+    if (UNIFORM) grp = (int64_t)__builtin_amdgcn_readfirstlane((int)grp);
+    const int64_t q0 = u - grp * part;
+    int64_t q[4];
+    bool has[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t qr = q0 + j * part;
+      has[j] = qr < P;
+      q[j] = has[j] ? qr : q0;
+    }
+    int64_t k_begin = grp, k_end = grp + 1;
+    if (SUM) {
+      k_begin = grp * p.chunk_keys;
+      k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
+    }
+    Block4 path[4];
+    int bi[4];
+    const int bb = p.bib;
+    const uint32_t bmask = (1u << bb) - 1u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t pi = p.shared_points ? q[j] : grp * P + q[j];
+      path[j] = load_block(p.tree_index + pi);
+      bi[j] = p.block_index ? p.block_index[pi] : (int)(path[j].w0 & bmask);
+    }
+    u128 acc[4] = {0, 0, 0, 0};
+    for (int64_t k = k_begin; k < k_end; ++k) {
+      const int party = p.party[k] & 1;
+      Block4 st[4];
+      uint32_t t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (p.seeds_in) {
+          const int64_t o = k * P + q[j];
+          st[j] = load_block(p.seeds_in + o);
+          t[j] = p.ctrl_in[o] & 1u;
+        } else {
+          st[j] = load_block(p.key_seed + k);
+          t[j] = (uint32_t)party;
+        }
+      }
+      const dpf_block* cws = p.cw_seed + k * p.cw_stride;
+      const uint8_t* cl = p.cw_left + k * p.cw_stride;
+      const uint8_t* cr = p.cw_right + k * p.cw_stride;
+      for (int lv = 0; lv < L; ++lv) {
+        uint32_t b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = path_bit(path[j], L - 1 - lv + bb);
+        const dpf_block c = cws[lv];
+        const uint32_t cctl = (uint32_t)(cl[lv] & 1) | ((uint32_t)(cr[lv] & 1) << 1);
+        const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
+                                    (uint32_t)(c.high >> 32));
+        path_stepN<4>(lk, p.rkl, p.rkd, st, t, b, cs, cctl);
+      }
+      dpf_aes::mmo_hashN<4>(st, lk, rv);
+      const dpf_block* vcw = p.vcw + k * p.vcw_stride;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const u128 v = fast_point_value<BITS>(st[j], t[j], bi[j], dpf_u128(vcw[bi[j]]), party,
+                                              p.xor_mode);
+        if (SUM) {
+          acc[j] = p.xor_mode ? (acc[j] ^ v) : (acc[j] + v);
+        } else if (has[j]) {
+          store_bits<BITS>(p.out + (k * P + q[j]) * (int64_t)p.esz, v);
+        }
+      }
+    }
+    if (SUM && k_begin < k_end) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!has[j]) continue;
+        unsigned long long* w = p.wide + q[j] * 3;
+        if (p.xor_mode) wide_xor(w, acc[j]); else wide_add(w, acc[j]);
+      }
+    }
+  }
+}
+
 // Counts points >= 2^log_domain_size (EvaluateAt's range check, h:861-874).
 __global__ void count_out_of_range_kernel(int64_t n, const dpf_block* __restrict__ pts, int log,
                                           unsigned long long* __restrict__ bad) {
@@ -608,6 +727,26 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
       else
         hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, false, false, false>), grid,
                            block, 0, s, p, leaf);
+      HIP_TRY(hipGetLastError());
+      return kOk;
+    }
+  }
+  if constexpr (FAST && !SUM) {
+    // Quads (ILP4) only on request (DPF_POINTS_QUAD=1): at config 4 they
+    // measured 674 M points/s against the pairs' 726 M.
+    const char* env = getenv("DPF_POINTS_QUAD");
+    const int64_t groups = pp.num_items / pp.half;
+    const int64_t part = (pp.points_per_key + 3) / 4;
+    if (env && env[0] == '1') {
+      PointParams p = pp;
+      p.half = part;
+      p.num_items = groups * part;
+      const int blk = block_for(p.num_items);
+      const dim3 grid(grid_for(p.num_items, blk)), block(blk);
+      if (part % 64 == 0)
+        hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM>), grid, block, 0, s, p);
+      else
+        hipLaunchKernelGGL((eval_points4_kernel<BITS, false, SUM>), grid, block, 0, s, p);
       HIP_TRY(hipGetLastError());
       return kOk;
     }

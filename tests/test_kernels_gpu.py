@@ -271,3 +271,17 @@ def test_eval_points_from_partials(hip):
                                     (("xor", 128), 40001), (GENERIC_TYPES[0], 33001)], ids=str)
 def test_eval_points_pairing_threshold(hip, vt, ppk):
     _points_case(hip, np.random.default_rng(ppk), vt, 1, ppk, 20)
+
+
+# The quad (four chains per lane) point kernel, forced on at small sizes:
+# ragged P (P % 4 != 0, P < 4), wave-uniform parts (P = 256, 1024) and partials.
+@pytest.mark.parametrize("vt,num_keys,ppk,levels,partials", [
+    (("int", 64), 1, 777, 20, False), (("int", 64), 37, 64, 63, False),
+    (("int", 64), 9, 256, 1, False), (("int", 32), 3, 1024, 30, False),
+    (("int", 128), 5, 6, 127, False), (("xor", 128), 5, 100, 12, True),
+    (("int", 8), 4, 5, 0, False), (("int", 16), 2, 3, 9, False),
+    (("xor", 64), 11, 13, 40, True)], ids=str)
+def test_eval_points_quad(hip, monkeypatch, vt, num_keys, ppk, levels, partials):
+    monkeypatch.setenv("DPF_POINTS_QUAD", "1")
+    _points_case(hip, np.random.default_rng(ppk * 31 + levels), vt, num_keys, ppk, levels,
+                 from_partials=partials)
