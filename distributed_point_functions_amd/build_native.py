@@ -44,7 +44,7 @@ HIP_FLAGS = [
 # (batch_level_kernel<Mod32V, 2, true>, 128 VGPRs).
 # dpf_expand_hybrid.hip: the bitsliced rounds need the default scheduler's
 # register discipline (iterative-ilp: 228 VGPRs vs 175 at 2 waves per SIMD).
-DEFAULT_SCHED_TUS = {"dpf_batch.hip", "dpf_expand_hybrid.hip"}
+DEFAULT_SCHED_TUS = {"dpf_batch.hip", "dpf_expand_hybrid.hip", "dpf_expand_ws.hip"}
 
 
 def _run(cmd, cwd=ROOT):

@@ -1066,6 +1066,34 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
     return launch_expand_hybrid(num_starts, seeds_in, control_in, num_levels, cw_seed, cw_left,
                                 cw_right, key_left, key_right, key_value, desc, value_correction,
                                 party, out, (hipStream_t)stream);
+  // Integer leaves filling whole blocks: the wave-specialised kernel when it is
+  // enabled (DPF_EXPAND_WS=1, opt-in) and the tree gives every tree lane a
+  // subtree (dpf_expand_ws.hip).
+  {
+    int bits = 0, lanes = 0, sb = 0, kind = 0;
+    if (fast_int(desc)) {
+      bits = desc->bits[0];
+      lanes = desc->elements_per_block;
+      sb = elements_per_leaf * bits / 8;
+      kind = desc->kind[0];
+    } else if (desc->direct && desc->blocks_needed == 1) {
+      bool uniform = true;
+      for (int k = 1; k < desc->num_leaves; ++k)
+        uniform = uniform && desc->bits[k] == desc->bits[0] && desc->kind[k] == desc->kind[0];
+      if (uniform && desc->kind[0] != DPF_LEAF_INTMODN &&
+          desc->elements_per_block * desc->num_leaves * desc->bits[0] <= 128) {
+        bits = desc->bits[0];
+        lanes = desc->elements_per_block * desc->num_leaves;
+        sb = elements_per_leaf * packed_size(desc);
+        kind = desc->kind[0];
+      }
+    }
+    if (sb == 16 && expand_ws_applies(num_starts, num_levels, key_value))
+      return launch_expand_ws(num_starts, seeds_in, control_in, num_levels, cw_seed, cw_left,
+                              cw_right, key_left, key_right, key_value, bits,
+                              kind == DPF_LEAF_XOR, lanes, value_correction, party, out,
+                              (hipStream_t)stream);
+  }
   // Choose the depth-first subtree depth S and the per-item walk depth k0.
   const int64_t threads = (int64_t)num_cus() * kWgPerCu * kBlock;
   int S = num_levels < kSMax ? num_levels : kSMax;

@@ -38,6 +38,18 @@ int launch_expand_hybrid(int64_t num_starts, const dpf_block* seeds_in, const ui
                          const dpf_value_desc* desc, const dpf_block* value_correction, int party,
                          void* out, hipStream_t s);
 
+// dpf_expand_ws.hip: full-domain expansion in wave-specialised workgroups (12
+// T-table tree waves + 4 bitsliced value waves per CU) for integer leaves that
+// fill whole 16-byte blocks, the reference's value key, and at least one
+// subtree of depth >= 5 per tree lane.
+bool expand_ws_applies(int64_t num_starts, int num_levels, const dpf_aes_key* key_value);
+int launch_expand_ws(int64_t num_starts, const dpf_block* seeds_in, const uint8_t* control_in,
+                     int num_levels, const dpf_block* cw_seed, const uint8_t* cw_left,
+                     const uint8_t* cw_right, const dpf_aes_key* key_left,
+                     const dpf_aes_key* key_right, const dpf_aes_key* key_value, int bits,
+                     bool xor_leaf, int elements, const dpf_block* value_correction, int party,
+                     void* out, hipStream_t s);
+
 }  // namespace dpf_rt
 
 #define HIP_TRY(expr)                                           \

@@ -195,6 +195,52 @@ def test_expand_hybrid_shapes(hip, vt, levels, n0, party, monkeypatch):
     _expand_case(hip, rng, vt, n0, levels, party)
 
 
+# The opt-in wave-specialised kernel (DPF_EXPAND_WS=1, dpf_expand_ws.hip) for
+# integer leaves filling whole blocks once every tree lane of a full launch
+# (256 CUs x 768) gets a subtree of depth >= 5: 12 T-table waves per CU expand
+# the tree and hand half-octets of leaf seeds through LDS slots to 4 bitsliced
+# waves.
+# Shapes: (23, 1) runs rounds at depths 5, 3, 3; (24, 3) exactly one round;
+# (22, 7) a last round of 2^17 lanes; (6, 196645) a last round whose final
+# wave is partly idle (148 subtrees of depth 4).
+WS_SHAPES = [(23, 1), (24, 3), (22, 7), (6, 196645)]
+
+
+@pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
+@pytest.mark.parametrize("levels,n0", WS_SHAPES)
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_ws_shapes(hip, vt, levels, n0, party, monkeypatch):
+    if (levels, n0) != (23, 1) and vt not in (("int", 64), ("xor", 128), ("int", 8)):
+        pytest.skip("shape covered by the other types")
+    monkeypatch.setenv("DPF_EXPAND_WS", "1")
+    rng = np.random.default_rng(hash((str(vt), levels, n0, party, "ws")) & 0xFFFFFFFF)
+    _expand_case(hip, rng, vt, n0, levels, party)
+
+
+@pytest.mark.parametrize("levels,n0", [(23, 1), (6, 196645)])
+def test_expand_ws_matches_octet_kernel(hip, levels, n0, monkeypatch):
+    # Same inputs through the wave-specialised and the octet kernel.
+    import torch
+    vt = ("int", 64)
+    rng = np.random.default_rng(levels * 1000 + n0)
+    seeds = _rand_blocks(rng, n0)
+    ctrl = rng.integers(0, 2, size=n0, dtype=np.uint8)
+    cws = _rand_blocks(rng, levels)
+    cl = rng.integers(0, 2, size=levels, dtype=np.uint8)
+    cr = rng.integers(0, 2, size=levels, dtype=np.uint8)
+    vcw = [_rand_value(rng, vt) for _ in range(2)]
+    args = (hip.to_device_blocks(seeds), hip.to_device_u8(ctrl), hip.to_device_blocks(cws),
+            hip.to_device_u8(cl), hip.to_device_u8(cr),
+            (O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE), _desc(hip, vt, 1), 2,
+            hip.to_device_blocks(O._leaf_array(vcw)), 1)
+    monkeypatch.setenv("DPF_EXPAND_WS", "1")
+    ws = hip.expand(*args)
+    monkeypatch.setenv("DPF_EXPAND_WS", "0")
+    octet = hip.expand(*args)
+    torch.cuda.synchronize()
+    assert torch.equal(ws, octet)
+
+
 @pytest.mark.parametrize("vt,cepb", [(("int", 8), 1), (("int", 8), 4), (("int", 16), 2),
                                      (("int", 32), 1), (("int", 64), 1)], ids=str)
 def test_expand_partial_blocks(hip, vt, cepb):

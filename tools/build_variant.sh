@@ -11,7 +11,7 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -Iinclude"
 for src in $K/*.hip; do
   b=$(basename $src .hip)
   sched="-mllvm -amdgpu-sched-strategy=iterative-ilp"
-  { [ "$b" = dpf_batch ] || [ "$b" = dpf_expand_hybrid ]; } && sched=""
+  { [ "$b" = dpf_batch ] || [ "$b" = dpf_expand_hybrid ] || [ "$b" = dpf_expand_ws ]; } && sched=""
   /opt/rocm/bin/hipcc $F $sched "$@" -c $src -o $out/$b.o &
 done
 wait
