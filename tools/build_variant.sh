@@ -10,7 +10,7 @@ K=distributed_point_functions_amd/csrc/kernels
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -Iinclude"
 for src in $K/*.hip; do
   b=$(basename $src .hip)
-  sched="-mllvm -amdgpu-sched-strategy=iterative-ilp"
+  sched="-mllvm -amdgpu-sched-strategy=${DPF_SCHED:-iterative-ilp}"
   { [ "$b" = dpf_batch ] || [ "$b" = dpf_expand_hybrid ] || [ "$b" = dpf_expand_ws ]; } && sched=""
   /opt/rocm/bin/hipcc $F $sched "$@" -c $src -o $out/$b.o &
 done
