@@ -29,6 +29,10 @@
 #else
 #define DPF_UNROLL
 #endif
+// Last-round scheduling fence every DPF_LAST_ROUND_FENCE chains (encryptN).
+#ifndef DPF_LAST_ROUND_FENCE
+#define DPF_LAST_ROUND_FENCE 2
+#endif
 #if defined(DPF_AES_UNROLL_ROUNDS)
 #define DPF_ROUND_LOOP _Pragma("unroll")
 #else
@@ -244,11 +248,19 @@ DPF_UNROLL
     return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ k;
   };
 DPF_UNROLL
-  for (int i = 0; i < N; ++i)
+  for (int i = 0; i < N; ++i) {
     st[i] = Block4{last(w[i][0], w[i][1], w[i][2], w[i][3], rk[i](40)),
                    last(w[i][1], w[i][2], w[i][3], w[i][0], rk[i](41)),
                    last(w[i][2], w[i][3], w[i][0], w[i][1], rk[i](42)),
                    last(w[i][3], w[i][0], w[i][1], w[i][2], rk[i](43))};
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Keeps the scheduler from issuing all N chains' last-round lookups before
+    // any is consumed: at ILP4 the 64 live results spilled at 128 VGPRs (the
+    // octet kernel: 37 -> 23 spilled VGPRs, HBM traffic 21.5 -> 17.7 GB per
+    // config-2 launch, same speed; profiles/r11_ws_ab.txt).
+    if (i % DPF_LAST_ROUND_FENCE == DPF_LAST_ROUND_FENCE - 1) __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
 }
 
 // N MMO hashes interleaved.

@@ -261,8 +261,10 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
         node = c0;
         nt = t0;
       }
+#if !defined(DPF_LATE_PREFETCH)
       // The next octet's root (written by now), loaded an octet ahead.
       if (g + 1 < ngroups) next = sib[G - (int)__builtin_ctzll((unsigned long long)(g + 1)) - 1];
+#endif
       // 3. the octet.
       const int lvl = k0 + G;
       Block4 c[2], q[4];
@@ -271,6 +273,11 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
                     ct[0], c[1], ct[1]);
       children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
                        lds.cw_ctrl[lvl + 1], q, qt);
+#if defined(DPF_LATE_PREFETCH)
+      // The next octet's root (written by now), loaded half an octet ahead:
+      // not live across the grandchildren's hashes.
+      if (g + 1 < ngroups) next = sib[G - (int)__builtin_ctzll((unsigned long long)(g + 1)) - 1];
+#endif
       uint4* o = reinterpret_cast<uint4*>(p.out + (leaf_base + 8 * g) * 16);
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
@@ -1094,12 +1101,31 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
                               kind == DPF_LEAF_XOR, lanes, value_correction, party, out,
                               (hipStream_t)stream);
   }
-  // Choose the depth-first subtree depth S and the per-item walk depth k0.
-  const int64_t threads = (int64_t)num_cus() * kWgPerCu * kBlock;
+  // Choose the depth-first subtree depth S (items = num_starts * 2^(L - S)
+  // subtrees, each walked k0 = L - S levels from its start seed) by the
+  // per-thread critical path: rounds of items over the launch's threads times
+  // the AES of one item, the ILP1 walk counted twice.  Small trees get shallow
+  // subtrees and more items, so a launch far below one workgroup per CU is not
+  // serialised on a few lanes' DFS; start counts that are not powers of two
+  // (5 starts x 2^27: 1.25 subtrees of depth 11 per thread = 2 rounds) get
+  // subtrees shallow enough to divide evenly (depth 9: 5 rounds of 1, +53%).
   int S = num_levels < kSMax ? num_levels : kSMax;
-  // Small trees: shallow subtrees and more items, so that a launch far below
-  // one full workgroup per CU is not serialised on a few lanes' DFS.
-  while (S > 1 && (num_starts << (num_levels - S)) < threads) --S;
+  {
+    double best = -1;
+    int best_s = S;
+    for (int cand = S; cand >= (num_levels > 0 ? 1 : 0); --cand) {
+      const int64_t items = num_starts << (num_levels - cand);
+      const int blk = block_for(items);
+      const int64_t threads = (int64_t)grid_for(items, blk) * blk;
+      const int64_t rounds = (items + threads - 1) / threads;
+      const double cost = (double)rounds * (2.0 * (num_levels - cand) + 3.0 * (double)(1ll << cand));
+      if (best < 0 || cost < best * 0.999) {
+        best = cost;
+        best_s = cand;
+      }
+    }
+    S = best_s;
+  }
 #if defined(DPF_FORCE_S)
   if (num_levels >= DPF_FORCE_S) S = DPF_FORCE_S;  // variant builds (tools/variant_bench.py)
 #endif

@@ -195,6 +195,17 @@ def test_expand_hybrid_shapes(hip, vt, levels, n0, party, monkeypatch):
     _expand_case(hip, rng, vt, n0, levels, party)
 
 
+# Start counts that are not powers of two: dpf_hip_expand picks the subtree
+# depth by the per-thread critical path (5 starts x 2^21: depth 4, 5 * 2^17
+# subtrees in 3 even rounds, where "fill the launch" gave depth 5 in 2 rounds).
+@pytest.mark.parametrize("vt", [("int", 64), ("xor", 128), ("int", 32)], ids=str)
+@pytest.mark.parametrize("levels,n0", [(21, 5), (19, 11)])
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_uneven_starts(hip, vt, levels, n0, party):
+    rng = np.random.default_rng(hash((str(vt), levels, n0, party, "uneven")) & 0xFFFFFFFF)
+    _expand_case(hip, rng, vt, n0, levels, party)
+
+
 # The opt-in wave-specialised kernel (DPF_EXPAND_WS=1, dpf_expand_ws.hip) for
 # integer leaves filling whole blocks once every tree lane of a full launch
 # (256 CUs x 768) gets a subtree of depth >= 5: 12 T-table waves per CU expand
