@@ -184,10 +184,18 @@ __device__ __forceinline__ void ws_tree_item(WsLds& lds, const LdsLookup& lk, co
     children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.img.cw_seed[lvl + 1],
                      lds.img.cw_ctrl[lvl + 1], q, qt);
     const int64_t octet = octet_base + g;
+    // The second half's grandchildren wait in scratch (as in expand_octet_kernel).
+    static_assert(12 - 3 <= kGMax - 2, "stash overlaps the DFS stack");
+    sib[kGMax - 2] = q[2];
+    sib[kGMax - 1] = q[3];
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       Block4 l[4];
       uint32_t lt[4];
+      if (hf == 1) {
+        q[2] = sib[kGMax - 2];
+        q[3] = sib[kGMax - 1];
+      }
       children_step_x2(lk, p.rkl.k, p.rkr.k, q[2 * hf], qt[2 * hf], q[2 * hf + 1], qt[2 * hf + 1],
                        lds.img.cw_seed[lvl + 2], lds.img.cw_ctrl[lvl + 2], l, lt);
       const bool self = p.self_period > 0 && ((2 * g + hf) % p.self_period) == p.self_period - 1;

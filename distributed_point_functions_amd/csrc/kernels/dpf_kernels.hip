@@ -279,10 +279,22 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
       if (g + 1 < ngroups) next = sib[G - (int)__builtin_ctzll((unsigned long long)(g + 1)) - 1];
 #endif
       uint4* o = reinterpret_cast<uint4*>(p.out + (leaf_base + 8 * g) * 16);
+      // The second half's two grandchildren wait in scratch beside the DFS
+      // stack (two 16-byte stores and loads per octet) instead of 8 VGPRs
+      // across the first half: 128 VGPRs with 37 spilled -> 110 with none,
+      // +3.5% and HBM traffic 17.7 -> 12.1 GB per config-2 launch
+      // (profiles/r11_ws_ab.txt).  The DFS uses sib[0 .. S-4], S <= kSMax.
+      static_assert(kSMax - 3 <= kGMax - 2, "stash overlaps the DFS stack");
+      sib[kGMax - 2] = q[2];
+      sib[kGMax - 1] = q[3];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         Block4 l[4];
         uint32_t lt[4];
+        if (hf == 1) {
+          q[2] = sib[kGMax - 2];
+          q[3] = sib[kGMax - 1];
+        }
         children_step_x2(lk, p.rkl.k, p.rkr.k, q[2 * hf], qt[2 * hf], q[2 * hf + 1],
                          qt[2 * hf + 1], lds.cw_seed[lvl + 2], lds.cw_ctrl[lvl + 2], l, lt);
         dpf_aes::mmo_hashN<4>(l, lk, rv);
