@@ -261,10 +261,8 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
         node = c0;
         nt = t0;
       }
-#if !defined(DPF_LATE_PREFETCH)
       // The next octet's root (written by now), loaded an octet ahead.
       if (g + 1 < ngroups) next = sib[G - (int)__builtin_ctzll((unsigned long long)(g + 1)) - 1];
-#endif
       // 3. the octet.
       const int lvl = k0 + G;
       Block4 c[2], q[4];
@@ -273,11 +271,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
                     ct[0], c[1], ct[1]);
       children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
                        lds.cw_ctrl[lvl + 1], q, qt);
-#if defined(DPF_LATE_PREFETCH)
-      // The next octet's root (written by now), loaded half an octet ahead:
-      // not live across the grandchildren's hashes.
-      if (g + 1 < ngroups) next = sib[G - (int)__builtin_ctzll((unsigned long long)(g + 1)) - 1];
-#endif
       uint4* o = reinterpret_cast<uint4*>(p.out + (leaf_base + 8 * g) * 16);
       // The second half's two grandchildren wait in scratch beside the DFS
       // stack (two 16-byte stores and loads per octet) instead of 8 VGPRs
