@@ -213,9 +213,31 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
 // 8 GiB written).  Measured same-box at config 2: 18.58 vs 18.87-18.98 ms per
 // 2^30 outputs with identical outputs (tools/octet_check.py); in the bench
 // 17.9 ms per step (59.95 G leaves/s).
+// Half an octet's leaves (4 consecutive leaf blocks): integer leaves filling
+// whole blocks store 4 x 16 contiguous bytes; other policies use their emit4.
 template <int BITS, bool XOR>
-__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
-    ExpandParams p, FastIntLeaf<BITS, XOR> leaf) {
+__device__ __forceinline__ void octet_half(const FastIntLeaf<BITS, XOR>& leaf, const LdsLookup& lk,
+                                           const uint32_t* rkv, Block4* l, const uint32_t* lt,
+                                           int64_t first_leaf, char* out) {
+  const UniformRK rv[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
+  dpf_aes::mmo_hashN<4>(l, lk, rv);
+  uint4* o = reinterpret_cast<uint4*>(out + first_leaf * 16);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const Block4 h = leaf.correct(l[j], lt[j]);
+    o[j] = make_uint4(h.w0, h.w1, h.w2, h.w3);
+  }
+}
+template <class Leaf>
+__device__ __forceinline__ void octet_half(const Leaf& leaf, const LdsLookup& lk,
+                                           const uint32_t* rkv, Block4* l, const uint32_t* lt,
+                                           int64_t first_leaf, char* out) {
+  leaf.emit4(lk, rkv, l, lt, first_leaf, out);
+}
+
+template <class Leaf>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(ExpandParams p,
+                                                                             Leaf leaf) {
   __shared__ LdsImage lds;
   leaf.init();
   fill_tables(lds.tab);
@@ -225,8 +247,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
   const int k0 = p.k0, S = p.S;
   const int G = S - 3;
   const int64_t ngroups = (int64_t)1 << G;
-  const UniformRK rv[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
-                           UniformRK{p.rkv.k}};
   for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
        item += (int64_t)gridDim.x * blockDim.x) {
     // 1. walk from the start seed to this item's subtree root.
@@ -271,7 +291,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
                     ct[0], c[1], ct[1]);
       children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
                        lds.cw_ctrl[lvl + 1], q, qt);
-      uint4* o = reinterpret_cast<uint4*>(p.out + (leaf_base + 8 * g) * 16);
       // The second half's two grandchildren wait in scratch beside the DFS
       // stack (two 16-byte stores and loads per octet) instead of 8 VGPRs
       // across the first half: 128 VGPRs with 37 spilled -> 110 with none,
@@ -290,12 +309,9 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(
         }
         children_step_x2(lk, p.rkl.k, p.rkr.k, q[2 * hf], qt[2 * hf], q[2 * hf + 1],
                          qt[2 * hf + 1], lds.cw_seed[lvl + 2], lds.cw_ctrl[lvl + 2], l, lt);
-        dpf_aes::mmo_hashN<4>(l, lk, rv);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const Block4 h = leaf.correct(l[j], lt[j]);
-          o[4 * hf + j] = make_uint4(h.w0, h.w1, h.w2, h.w3);
-        }
+        // The half's four value hashes (ILP4), conversion, correction, stores
+        // (integer leaves: 64 contiguous bytes per lane).
+        octet_half(leaf, lk, p.rkv.k, l, lt, leaf_base + 8 * g + 4 * hf, p.out);
       }
     }
   }
@@ -705,8 +721,8 @@ bool launch_octet(const ExpandParams& p, const dpf_block* vcw, int E, int party,
   const char* off = getenv("DPF_EXPAND_NO_OCTET");
   if ((off && off[0] == '1') || store_bytes != 16 || p.S < 3) return false;
   const int blk = block_for(p.num_items);
-  hipLaunchKernelGGL((expand_octet_kernel<BITS, XOR>), dim3(grid_for(p.num_items, blk)), dim3(blk),
-                     0, s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
+  hipLaunchKernelGGL((expand_octet_kernel<FastIntLeaf<BITS, XOR>>), dim3(grid_for(p.num_items, blk)),
+                     dim3(blk), 0, s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
   return true;
 }
 
@@ -1197,6 +1213,14 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
           w.xmask |= (b >= 128 ? ~(u128)0 : (((u128)1 << b) - 1)) << off;
         off += b;
       }
+      const char* off_env = getenv("DPF_EXPAND_NO_OCTET");
+      if (p.S >= 3 && !(off_env && off_env[0] == '1')) {
+        const int blk = block_for(p.num_items);
+        hipLaunchKernelGGL((expand_octet_kernel<SwarLeaf>), dim3(grid_for(p.num_items, blk)),
+                           dim3(blk), 0, s, p, w);
+        HIP_TRY(hipGetLastError());
+        return kOk;
+      }
       return launch_expand(p, w, s);
     }
   }
@@ -1214,6 +1238,15 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
     if (desc->num_leaves <= 2) {
       Mod32Leaf<2> m;
       fill(m);
+      const char* off = getenv("DPF_EXPAND_NO_OCTET");
+      if (p.S >= 3 && !(off && off[0] == '1')) {
+        // Octet form (the half's four leaves hashed as two ILP4 groups).
+        const int blk = block_for(p.num_items);
+        hipLaunchKernelGGL((expand_octet_kernel<Mod32Leaf<2>>), dim3(grid_for(p.num_items, blk)),
+                           dim3(blk), 0, s, p, m);
+        HIP_TRY(hipGetLastError());
+        return kOk;
+      }
       return launch_expand(p, m, s);
     }
     Mod32Leaf<kMod32MaxLeaves> m;

@@ -18,7 +18,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run_one(reps, levels, starts):
+VALUES = {  # name: (leaves, elements per block, packed bytes per element)
+    "u64": ([(0, 64, 0)], 2, 8),
+    "t32_64": ([(0, 32, 0), (0, 64, 0)], 1, 12),   # Tuple<uint32_t, uint64_t>: SwarLeaf
+    "t16x3": ([(0, 16, 0)] * 3, 2, 6),             # Tuple<uint16_t x 3>: uniform lanes
+}
+
+
+def run_one(reps, levels, starts, value="u64"):
     import numpy as np
     import torch
     from distributed_point_functions_amd import hip_abi as H
@@ -33,16 +40,17 @@ def run_one(reps, levels, starts):
 
     keys = (0x5be037ccf6a03de5935f08d0a5b6a2fd, 0xef94b6aedebb026ce2ea1fe0f66f4d0b,
             0x05a5d1588c5423e346a31101b21d1c98)
-    desc = H.value_desc([(H.LEAF_INT, 64, 0)], True, 2, 1)
+    leaves, epb, esz = VALUES[value]
+    desc = H.value_desc(leaves, True, epb, 1)
     D = levels
     seeds = rand_blocks(starts)
     ctrl = torch.zeros(starts, dtype=torch.uint8, device=dev)
     cws = rand_blocks(D)
     cl = torch.randint(0, 2, (D,), dtype=torch.uint8, device=dev, generator=g)
     cr = torch.randint(0, 2, (D,), dtype=torch.uint8, device=dev, generator=g)
-    vcw = rand_blocks(2)
-    out = torch.empty(starts * (1 << (D + 1)) * 8, dtype=torch.uint8, device=dev)
-    fn = lambda: H.expand(seeds, ctrl, cws, cl, cr, keys, desc, 2, vcw, 0, out=out)  # noqa: E731
+    vcw = rand_blocks(epb * len(leaves))
+    out = torch.empty(starts * (1 << D) * epb * esz, dtype=torch.uint8, device=dev)
+    fn = lambda: H.expand(seeds, ctrl, cws, cl, cr, keys, desc, epb, vcw, 0, out=out)  # noqa: E731
     fn()
     torch.cuda.synchronize()
     ev = [(H.Event(), H.Event()) for _ in range(reps)]
@@ -64,10 +72,11 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--levels", type=int, default=29)
     ap.add_argument("--starts", type=int, default=1)
+    ap.add_argument("--value", default="u64", choices=sorted(VALUES))
     ap.add_argument("--one", action="store_true")
     a = ap.parse_args()
     if a.one:
-        return run_one(a.reps, a.levels, a.starts)
+        return run_one(a.reps, a.levels, a.starts, a.value)
     for _ in range(a.rounds):
         for v in a.variants:
             lib, _, envs = v.partition(":")
@@ -76,7 +85,8 @@ def main():
                 k, _, val = kv.partition("=")
                 env[k] = val
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--one", "--reps",
-                                str(a.reps), "--levels", str(a.levels), "--starts", str(a.starts)],
+                                str(a.reps), "--levels", str(a.levels), "--starts", str(a.starts),
+                                "--value", a.value],
                                env=env, capture_output=True, text=True, timeout=300)
             for line in r.stdout.splitlines():
                 if line.startswith("{"):
