@@ -51,7 +51,7 @@ AES_VALU_PEAK_GBLOCKS = 245.8
 AES_LDS_PEAK_GBLOCKS = 122.9
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
 METRIC = "DPF leaf evals/sec, full-domain 2^30 uint64 at 1/2/4/8 GPUs; AES blocks/s"
-KERNEL = "expand_octet_kernel<64, false>"
+KERNEL = "expand_octet_kernel<FastIntLeaf<64, false> >"
 
 
 def parse():
@@ -222,7 +222,9 @@ def profiled_traffic(kernel: str, leaves_per_launch: int = None):
             s = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if ("hbm_traffic_bytes" in s and kernel in s.get("kernel", "")
+        if ("hbm_traffic_bytes" in s
+                and kernel.replace("(anonymous namespace)::", "")
+                in s.get("kernel", "").replace("(anonymous namespace)::", "")
                 and (leaves_per_launch is None or s.get("leaves_per_launch") == leaves_per_launch)):
             best = (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT),
                     {"valu_lane_ops_per_aes": s.get("valu_lane_ops_per_aes"),
@@ -237,8 +239,8 @@ def profiled_traffic(kernel: str, leaves_per_launch: int = None):
 
 def kernel_name(args, bits: int) -> str:
     if args.workload == "full_domain_tuple":
-        return ("expand_kernel<Mod32Leaf<2> >" if args.tuple_type == "intmodn32x2"
-                else "expand_octet_kernel<32, false>")
+        return ("expand_octet_kernel<Mod32Leaf<2> >" if args.tuple_type == "intmodn32x2"
+                else "expand_octet_kernel<FastIntLeaf<32, false> >")
     return KERNEL.replace("64", str(bits))
 
 
@@ -379,7 +381,7 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = (profiled_traffic("expand_octet_kernel<64, false>", outputs_per_rank)
+        tr = (profiled_traffic(KERNEL, outputs_per_rank)
               if args.workload == "full_domain" else None)
         vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
                  "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "

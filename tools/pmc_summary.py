@@ -37,7 +37,7 @@ def main():
     durs = []
     for f in glob.glob(os.path.join(a.dir, "trace", "*kernel_trace.csv")):
         for row in csv.DictReader(open(f)):
-            if a.kernel in row["Kernel_Name"]:
+            if a.kernel in row["Kernel_Name"].replace("(anonymous namespace)::", ""):
                 durs.append((int(row["Grid_Size_X"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"]),
                              row["Kernel_Name"]))
     grid = max(g for g, _, _ in durs) if durs else None
@@ -48,7 +48,7 @@ def main():
     sums, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            if a.kernel in row["Kernel_Name"] and (a.total or int(row["Grid_Size"]) == grid):
+            if a.kernel in row["Kernel_Name"].replace("(anonymous namespace)::", "") and (a.total or int(row["Grid_Size"]) == grid):
                 c = row["Counter_Name"]
                 sums[c] += float(row["Counter_Value"])
                 launches[c].add(row["Dispatch_Id"])
