@@ -163,7 +163,18 @@ def run_cpu_pool(work, items, threads: int = CPU_THREADS, budget_s: float = 15.0
     return units, time.perf_counter() - t0, n_items
 
 
-def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
+def _leaf_ints(v) -> list:
+    """A proto Value flattened to its leaf integers (the oracle's value form)."""
+    which = v.WhichOneof("value")
+    if which == "tuple":
+        return [x for e in v.tuple.elements for x in _leaf_ints(e)]
+    iv = getattr(v, which)
+    if iv.WhichOneof("value") == "value_uint128":
+        return [iv.value_uint128.high << 64 | iv.value_uint128.low]
+    return [int(iv.value_uint64)]
+
+
+def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64, vt=None):
     """The oracle (C restatement of dpf/distributed_point_function.cc:271-349,
     OpenSSL AES-NI in 64-block batches) on the SAME workload, on CPU_THREADS host
     threads: the 2^24-output subtrees of the benchmark key, each walked to its
@@ -172,15 +183,18 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
     kept for the command line and unused."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    P = O.OracleParams([(log_domain, ("int", bits), 0)])
-    sub = 17 if bits == 64 else 18            # 2^18 outputs per work item
+    vt = vt or ("int", bits)
+    P = O.OracleParams([(log_domain, vt, 0)])
+    epb = O.elements_per_block(vt)
+    sub = 18 - (epb.bit_length() - 1)         # 2^18 outputs per work item
+    b = P.blocks_needed[0]
     T = P.hierarchy_to_tree[0]
     top = T - sub
     # The product DpfKey (proto) restated as the oracle's key dict.
     k = {"seed": key.seed.high << 64 | key.seed.low, "party": key.party,
          "cws": [(c.seed.high << 64 | c.seed.low, int(c.control_left), int(c.control_right),
                   None) for c in key.correction_words],
-         "last_vc": [[_int_of(v)] for v in key.last_level_value_correction]}
+         "last_vc": [_leaf_ints(v) for v in key.last_level_value_correction]}
     vcw = O._value_correction(P, k, 0)
     cs_top, cl_top, cr_top = O._cw_arrays(k, 0, top)
     cs, cl, cr = O._cw_arrays(k, top, T)
@@ -193,7 +207,7 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
                                       np.array([k["party"]], np.uint8),
                                       O.blocks_from_ints([c]), cs_top, cl_top, cr_top)
         es, ec = O.expand_seeds(seed, ctrl, cs, cl, cr)
-        return O.hash_correct(("int", bits), es, ec, 1, P.cepb(0), vcw, k["party"]).shape[0]
+        return O.hash_correct(vt, es, ec, b, P.cepb(0), vcw, k["party"]).shape[0]
 
     leaves, dt, done = run_cpu_pool(work, range(n_sub), budget_s=20.0)
     # SURVEY.md 8d also asks for the single-threaded rate (the reference is
@@ -203,11 +217,11 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64):
             "single_thread_value": leaves1 / dt1,
             "single_thread_sample": f"{done1} subtrees of 2^18 outputs, {dt1:.1f} s on 1 thread",
             "host": host_cpu(),
-            "sample": f"{done} of the {n_sub} subtrees of 2^18 uint{bits} outputs of the benchmark "
+            "sample": f"{done} of the {n_sub} subtrees of 2^18 {vt} outputs of the benchmark "
                       f"key (2^{log_domain} domain): EvaluateSeeds to each subtree root, then "
                       f"ExpandSeeds+HashExpandedSeeds+correction (oracle over OpenSSL AES-NI); "
                       f"{dt:.1f} s wall on {CPU_THREADS} host threads",
-            "aes_blocks_per_s": done * (tree_aes_per_launch(sub) + top) / dt}
+            "aes_blocks_per_s": done * (tree_aes_per_launch(sub, b) + top) / dt}
 
 
 def profiled_traffic(kernel: str, leaves_per_launch: int = None):
@@ -424,8 +438,12 @@ def main():
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS},
         }
-        if world == 1 and not args.no_cpu_baseline and args.workload != "full_domain_tuple":
-            res["cpu_baseline"] = cpu_baseline(key, log_domain, args.cpu_chunks, bits)
+        if world == 1 and not args.no_cpu_baseline:
+            ovt = None
+            if args.workload == "full_domain_tuple":
+                ovt = (("tuple", [("intmodn", 32, 4294967291)] * 2)
+                       if args.tuple_type == "intmodn32x2" else ("tuple", [("int", 32)] * 2))
+            res["cpu_baseline"] = cpu_baseline(key, log_domain, args.cpu_chunks, bits, vt=ovt)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -442,7 +460,7 @@ def _oracle_key(key):
     return {"seed": key.seed.high << 64 | key.seed.low, "party": key.party,
             "cws": [(c.seed.high << 64 | c.seed.low, int(c.control_left), int(c.control_right),
                      None) for c in key.correction_words],
-            "last_vc": [[_int_of(v)] for v in key.last_level_value_correction]}
+            "last_vc": [_leaf_ints(v) for v in key.last_level_value_correction]}
 
 
 def cpu_baseline_points(dpf, batch, host_points, keys: int, ppk: int):
