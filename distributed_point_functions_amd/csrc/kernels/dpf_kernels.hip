@@ -213,10 +213,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
 // 8 GiB written).  Measured same-box at config 2: 18.58 vs 18.87-18.98 ms per
 // 2^30 outputs with identical outputs (tools/octet_check.py); in the bench
 // 17.9 ms per step (59.95 G leaves/s).
-#ifndef DPF_OCTET_PRIO_SPLIT
-#define DPF_OCTET_PRIO_SPLIT 1
-#endif
-
 // Half an octet's leaves (4 consecutive leaf blocks): integer leaves filling
 // whole blocks store 4 x 16 contiguous bytes; other policies use their emit4.
 template <int BITS, bool XOR>
@@ -247,11 +243,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
   __syncthreads();
-#if DPF_OCTET_PRIO_SPLIT > 0
-  // Every other wave at a higher issue priority: the waves' LDS and VALU
-  // phases drift apart (+0.5% same-box, 3 of 3 rounds; priority 3: noise).
-  if ((threadIdx.x >> 6) & 1) __builtin_amdgcn_s_setprio(DPF_OCTET_PRIO_SPLIT);
-#endif
   const LdsLookup lk = make_lookup(lds);
   const int k0 = p.k0, S = p.S;
   const int G = S - 3;
