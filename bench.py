@@ -395,8 +395,8 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = (profiled_traffic(KERNEL, outputs_per_rank)
-              if args.workload == "full_domain" else None)
+        tr = (profiled_traffic(kernel_name(args, bits), outputs_per_rank)
+              if args.workload in ("full_domain", "full_domain_tuple") else None)
         vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
                  "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "
                                                       "IntModN<uint32_t, 4294967291>>",
