@@ -14,13 +14,18 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(2); } } while (0)
 
-template <int CH>
+// MODE 0: the T-table layout (32 copies, lane l -> copy l & 31, v_perm address).
+// MODE 1: 64 copies of one table, lane l -> copy l (lanes 32-63 on the other
+//         32 banks of the 64-bank array), v_perm address.
+// MODE 2: as 0 but ds_read_b64 (8-byte entries): instruction rate for 8 B/lane.
+template <int CH, int MODE>
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4, 4)))
 void lds_kernel(int iters, uint32_t* out, unsigned long long* clk) {
   __shared__ uint32_t tab[4 * 256 * 32];
   for (int i = threadIdx.x; i < 4 * 256 * 32; i += blockDim.x) tab[i] = i * 2654435761u;
   __syncthreads();
-  const uint32_t l = (threadIdx.x & 31) * 4u;
+  const uint32_t l = MODE == 1 ? (threadIdx.x & 63) * 4u : (MODE == 2 ? (threadIdx.x & 31) * 8u
+                                                                      : (threadIdx.x & 31) * 4u);
   const char* base = reinterpret_cast<const char*>(tab);
   uint32_t x[CH];
 #pragma unroll
@@ -31,8 +36,19 @@ void lds_kernel(int iters, uint32_t* out, unsigned long long* clk) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       // byte 2 of x as the entry, table T0 (low 64 KiB), copy l & 31
-      const uint32_t off = __builtin_amdgcn_perm(x[c], l, 0x0c020600u);
-      x[c] ^= *reinterpret_cast<const uint32_t*>(base + off);
+      if (MODE == 0) {
+        const uint32_t off = __builtin_amdgcn_perm(x[c], l, 0x0c020600u);
+        x[c] ^= *reinterpret_cast<const uint32_t*>(base + off);
+      } else if (MODE == 1) {
+        // 64 copies x 4 B = 256-byte rows: entry in bits 8-15 (128 rows: 32 KiB... x 2)
+        const uint32_t off = __builtin_amdgcn_perm(x[c], l, 0x0c020600u) & 0xffffu;
+        x[c] ^= *reinterpret_cast<const uint32_t*>(base + off);
+      } else {
+        // 32 copies x 8 B = 256-byte rows
+        const uint32_t off = __builtin_amdgcn_perm(x[c], l, 0x0c020600u) & 0xfff8u;
+        const uint2 v = *reinterpret_cast<const uint2*>(base + off);
+        x[c] ^= v.x ^ v.y;
+      }
     }
   }
   uint32_t a = 0;
@@ -46,7 +62,7 @@ void lds_kernel(int iters, uint32_t* out, unsigned long long* clk) {
   }
 }
 
-template <int CH>
+template <int CH, int MODE>
 void run(int cus) {
   uint32_t* d;
   unsigned long long* c;
@@ -59,7 +75,7 @@ void run(int cus) {
   float best = 1e30f;
   for (int r = 0; r < 4; ++r) {
     CK(hipEventRecord(a));
-    hipLaunchKernelGGL(lds_kernel<CH>, dim3(cus), dim3(1024), 0, 0, iters, d, c);
+    hipLaunchKernelGGL((lds_kernel<CH, MODE>), dim3(cus), dim3(1024), 0, 0, iters, d, c);
     CK(hipGetLastError());
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
@@ -72,8 +88,8 @@ void run(int cus) {
   const double ghz = (double)h[0] / ((double)h[1] / 100e6) / 1e9;
   const double lookups = (double)cus * 1024 * iters * CH;
   const double per_s = lookups / (best * 1e-3);
-  printf("{\"chains\": %d, \"ms\": %.3f, \"t_lookups_per_s\": %.2f, \"clock_ghz\": %.3f, "
-         "\"lane_lookups_per_clk_per_cu\": %.2f}\n", CH, best, per_s / 1e12, ghz,
+  printf("{\"mode\": %d, \"chains\": %d, \"ms\": %.3f, \"t_lookups_per_s\": %.2f, \"clock_ghz\": %.3f, "
+         "\"lane_lookups_per_clk_per_cu\": %.2f}\n", MODE, CH, best, per_s / 1e12, ghz,
          per_s / cus / (ghz * 1e9));
   CK(hipFree(d));
   CK(hipFree(c));
@@ -82,8 +98,12 @@ void run(int cus) {
 int main() {
   int cus = 256;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  run<4>(cus);
-  run<8>(cus);
-  run<16>(cus);
+  run<4, 0>(cus);
+  run<8, 0>(cus);
+  run<16, 0>(cus);
+  run<8, 1>(cus);
+  run<16, 1>(cus);
+  run<8, 2>(cus);
+  run<16, 2>(cus);
   return 0;
 }
