@@ -235,10 +235,29 @@ __device__ __forceinline__ void octet_half(const Leaf& leaf, const LdsLookup& lk
   leaf.emit4(lk, rkv, l, lt, first_leaf, out);
 }
 
+// Where the octet keeps its second half's two grandchildren during the first
+// half: 0 = both in scratch beside the DFS stack, 1 = q[3] in LDS (16 B per
+// lane), 2 = also q[2]'s upper 12 bytes in LDS, its low word in a VGPR -- the
+// LDS left over by the T-tables and correction words (150 + 12 KiB of 160).
+// Config 2: 17.21 -> 17.08 (1) -> 16.96 ms (2), WRITE_SIZE 1.30 -> 1.21 -> 1.18x
+// the 8 GiB written; SwarLeaf runs out of VGPRs at 2 (profiles/r11_ws_ab.txt).
+#ifndef DPF_OCTET_LDS_STASH
+#define DPF_OCTET_LDS_STASH 2
+#endif
+template <class Leaf> struct OctetStash { static constexpr int value = DPF_OCTET_LDS_STASH; };
+template <> struct OctetStash<SwarLeaf> {
+  static constexpr int value = DPF_OCTET_LDS_STASH < 1 ? DPF_OCTET_LDS_STASH : 1;
+};
+
 template <class Leaf>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(ExpandParams p,
                                                                              Leaf leaf) {
   __shared__ LdsImage lds;
+  constexpr int kStash = OctetStash<Leaf>::value;
+  __shared__ uint4 stash[kStash >= 1 ? kBlock : 1];
+  __shared__ uint3 stash2[kStash >= 2 ? kBlock : 1];
+  static_assert(sizeof(LdsImage) + (kStash >= 1 ? 16 * kBlock : 0) +
+                    (kStash >= 2 ? 12 * kBlock : 0) <= 160 * 1024, "LDS over 160 KiB");
   leaf.init();
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
@@ -291,21 +310,41 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
                     ct[0], c[1], ct[1]);
       children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
                        lds.cw_ctrl[lvl + 1], q, qt);
-      // The second half's two grandchildren wait in scratch beside the DFS
-      // stack (two 16-byte stores and loads per octet) instead of 8 VGPRs
-      // across the first half: 128 VGPRs with 37 spilled -> 110 with none,
-      // +3.5% and HBM traffic 17.7 -> 12.1 GB per config-2 launch
-      // (profiles/r11_ws_ab.txt).  The DFS uses sib[0 .. S-4], S <= kSMax.
+      // The second half's two grandchildren wait outside the VGPRs during the
+      // first half (OctetStash: lane-private LDS slots, else scratch beside
+      // the DFS stack) instead of 8 VGPRs: 128 VGPRs with 37 spilled -> 110
+      // with none, +3.5%, HBM traffic 17.7 -> 12.1 GB per config-2 launch in
+      // scratch, 10.9 GB in LDS (profiles/r11_ws_ab.txt).  The DFS uses
+      // sib[0 .. S-4], S <= kSMax.  Each lane reads back only its own slot.
       static_assert(kSMax - 3 <= kGMax - 2, "stash overlaps the DFS stack");
-      sib[kGMax - 2] = q[2];
-      sib[kGMax - 1] = q[3];
+      uint32_t q2w0 = 0;
+      if constexpr (kStash >= 2) {
+        q2w0 = q[2].w0;
+        stash2[threadIdx.x] = make_uint3(q[2].w1, q[2].w2, q[2].w3);
+      } else {
+        sib[kGMax - 2] = q[2];
+      }
+      if constexpr (kStash >= 1)
+        stash[threadIdx.x] = make_uint4(q[3].w0, q[3].w1, q[3].w2, q[3].w3);
+      else
+        sib[kGMax - 1] = q[3];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
         Block4 l[4];
         uint32_t lt[4];
         if (hf == 1) {
-          q[2] = sib[kGMax - 2];
-          q[3] = sib[kGMax - 1];
+          if constexpr (kStash >= 2) {
+            const uint3 u = stash2[threadIdx.x];
+            q[2] = Block4{q2w0, u.x, u.y, u.z};
+          } else {
+            q[2] = sib[kGMax - 2];
+          }
+          if constexpr (kStash >= 1) {
+            const uint4 v = stash[threadIdx.x];
+            q[3] = Block4{v.x, v.y, v.z, v.w};
+          } else {
+            q[3] = sib[kGMax - 1];
+          }
         }
         children_step_x2(lk, p.rkl.k, p.rkr.k, q[2 * hf], qt[2 * hf], q[2 * hf + 1],
                          qt[2 * hf + 1], lds.cw_seed[lvl + 2], lds.cw_ctrl[lvl + 2], l, lt);
