@@ -562,8 +562,18 @@ struct Mod32Leaf {
     for (int i = 0; i < NLMAX; ++i) c[i] = i < nl ? (uint32_t)vcw_elems[i].low : 0u;
   }
   __device__ __forceinline__ void convert_store(const uint32_t* w, uint32_t t, char* o) const {
-    uint32_t blk[4] = {w[0], w[1], w[2], w[3]};
     uint32_t x[NLMAX];
+    convert(w, t, x);
+    if (NLMAX >= 2 && nl == 2) {
+      *reinterpret_cast<uint2*>(o) = make_uint2(x[0], x[NLMAX >= 2 ? 1 : 0]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NLMAX; ++i)
+        if (i < nl) reinterpret_cast<uint32_t*>(o)[i] = x[i];
+    }
+  }
+  __device__ __forceinline__ void convert(const uint32_t* w, uint32_t t, uint32_t* x) const {
+    uint32_t blk[4] = {w[0], w[1], w[2], w[3]};
 #pragma unroll
     for (int i = 0; i < NLMAX; ++i) {
       if (i < nl) {
@@ -577,14 +587,9 @@ struct Mod32Leaf {
         if (party == 1) r = r == 0 ? 0u : n - r;
         x[i] = r;
         blk[0] = w[4 + i]; blk[1] = q[0]; blk[2] = q[1]; blk[3] = q[2];
+      } else {
+        x[i] = 0;
       }
-    }
-    if (NLMAX >= 2 && nl == 2) {
-      *reinterpret_cast<uint2*>(o) = make_uint2(x[0], x[NLMAX >= 2 ? 1 : 0]);
-    } else {
-#pragma unroll
-      for (int i = 0; i < NLMAX; ++i)
-        if (i < nl) reinterpret_cast<uint32_t*>(o)[i] = x[i];
     }
   }
   __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
@@ -601,33 +606,58 @@ struct Mod32Leaf {
     w[4] = h1.w0; w[5] = h1.w1; w[6] = h1.w2; w[7] = h1.w3;
     convert_store(w, t, out + leaf * 4 * nl);
   }
+  // The value blocks (seed, seed + 1) of two leaves as words w0[8], w1[8]
+  // (b == 2: one interleaved quadruple of hashes).
+  __device__ __forceinline__ void hash2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+                                        Block4 s1, uint32_t (&w0)[8], uint32_t (&w1)[8]) const {
+    Block4 h[4] = {s0, add_small(s0, 1u), s1, add_small(s1, 1u)};
+    if (b == 2) {
+      const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
+      dpf_aes::mmo_hashN<4>(h, lk, rk);
+    } else {
+      dpf_aes::mmo_hash2(h[0], h[2], lk, UniformRK{rkv}, UniformRK{rkv});
+      h[1] = h[3] = Block4{0, 0, 0, 0};
+    }
+    w0[0] = h[0].w0; w0[1] = h[0].w1; w0[2] = h[0].w2; w0[3] = h[0].w3;
+    w0[4] = h[1].w0; w0[5] = h[1].w1; w0[6] = h[1].w2; w0[7] = h[1].w3;
+    w1[0] = h[2].w0; w1[1] = h[2].w1; w1[2] = h[2].w2; w1[3] = h[2].w3;
+    w1[4] = h[3].w0; w1[5] = h[3].w1; w1[6] = h[3].w2; w1[7] = h[3].w3;
+  }
   __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
                                         uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
                                         char* out) const {
     uint32_t w0[8], w1[8];
-    if (b == 2) {
-      // Both leaves' two blocks (seed, seed + 1) as one interleaved quadruple.
-      Block4 h[4] = {s0, add_small(s0, 1u), s1, add_small(s1, 1u)};
-      const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
-      dpf_aes::mmo_hashN<4>(h, lk, rk);
-      w0[0] = h[0].w0; w0[1] = h[0].w1; w0[2] = h[0].w2; w0[3] = h[0].w3;
-      w0[4] = h[1].w0; w0[5] = h[1].w1; w0[6] = h[1].w2; w0[7] = h[1].w3;
-      w1[0] = h[2].w0; w1[1] = h[2].w1; w1[2] = h[2].w2; w1[3] = h[2].w3;
-      w1[4] = h[3].w0; w1[5] = h[3].w1; w1[6] = h[3].w2; w1[7] = h[3].w3;
-    } else {
-      dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{rkv}, UniformRK{rkv});
-      w0[0] = s0.w0; w0[1] = s0.w1; w0[2] = s0.w2; w0[3] = s0.w3;
-      w1[0] = s1.w0; w1[1] = s1.w1; w1[2] = s1.w2; w1[3] = s1.w3;
-#pragma unroll
-      for (int i = 4; i < 8; ++i) w0[i] = w1[i] = 0;
-    }
+    hash2(lk, rkv, s0, s1, w0, w1);
     convert_store(w0, t0, out + leaf * 4 * nl);
     convert_store(w1, t1, out + (leaf + 1) * 4 * nl);
   }
+  // Four consecutive leaves (leaf % 4 == 0), converted first and stored as
+  // whole 16-byte pieces: 32 contiguous bytes per lane for pairs (nl == 2),
+  // 16 for single elements -- not four 8-byte stores spread over the AES work.
   __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
                                         const uint32_t* t, int64_t leaf, char* out) const {
-    emit2(lk, rkv, s[0], t[0], s[1], t[1], leaf, out);
-    emit2(lk, rkv, s[2], t[2], s[3], t[3], leaf + 2, out);
+    uint32_t x[4][NLMAX];
+#pragma unroll
+    for (int j = 0; j < 4; j += 2) {
+      uint32_t w0[8], w1[8];
+      hash2(lk, rkv, s[j], s[j + 1], w0, w1);
+      convert(w0, t[j], x[j]);
+      convert(w1, t[j + 1], x[j + 1]);
+    }
+    if (NLMAX >= 2 && nl == 2) {
+      constexpr int i1 = NLMAX >= 2 ? 1 : 0;
+      uint4* o = reinterpret_cast<uint4*>(out + leaf * 8);
+      o[0] = make_uint4(x[0][0], x[0][i1], x[1][0], x[1][i1]);
+      o[1] = make_uint4(x[2][0], x[2][i1], x[3][0], x[3][i1]);
+    } else if (nl == 1) {
+      *reinterpret_cast<uint4*>(out + leaf * 4) = make_uint4(x[0][0], x[1][0], x[2][0], x[3][0]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < NLMAX; ++i)
+          if (i < nl) reinterpret_cast<uint32_t*>(out + (leaf + j) * 4 * nl)[i] = x[j][i];
+    }
   }
 };
 

@@ -18,12 +18,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-VALUES = {  # name: (leaves, elements per block, packed bytes per element[, blocks needed])
+VALUES = {  # name: (leaves, elements per block, packed bytes per element[, blocks needed, direct])
     "u64": ([(0, 64, 0)], 2, 8),
     "t32_64": ([(0, 32, 0), (0, 64, 0)], 1, 12),   # Tuple<uint32_t, uint64_t>: SwarLeaf
     "t16x3": ([(0, 16, 0)] * 3, 2, 6),             # Tuple<uint16_t x 3>: uniform lanes
     # Tuple<IntModN<uint32_t, 2^32 - 5> x 2>: Mod32Leaf, two value blocks per leaf
-    "m32x2": ([(1, 32, 4294967291)] * 2, 1, 8, 2),
+    "m32x2": ([(1, 32, 4294967291)] * 2, 1, 8, 2, False),
 }
 
 
@@ -42,9 +42,9 @@ def run_one(reps, levels, starts, value="u64"):
 
     keys = (0x5be037ccf6a03de5935f08d0a5b6a2fd, 0xef94b6aedebb026ce2ea1fe0f66f4d0b,
             0x05a5d1588c5423e346a31101b21d1c98)
-    leaves, epb, esz, *bn = VALUES[value]
-    bn = bn[0] if bn else 1
-    desc = H.value_desc(leaves, True, epb, bn)
+    leaves, epb, esz, *rest = VALUES[value]
+    bn = rest[0] if rest else 1
+    desc = H.value_desc(leaves, rest[1] if len(rest) > 1 else True, epb, bn)
     D = levels
     seeds = rand_blocks(starts)
     ctrl = torch.zeros(starts, dtype=torch.uint8, device=dev)
