@@ -22,6 +22,12 @@ path-walks the top k tree levels along the bits of r and expands its own
 2^30-output subtree.  No collective on the data path; one all_reduce(MAX) of
 the step time outside the timed region.
 
+`--host-output` (configs 2 and 3) adds `api_level`: the reference's own call
+shape, EvaluateUntil<uint64_t / absl::uint128>(0, {}, ctx) returning a
+std::vector in host memory (the device kernel + a bounce-buffered D2H copy
+into the caller's vector), timed on the same key -- PCIe-inclusive, reported
+beside the kernel-level number and never as `value`.
+
 Run: python bench.py [--gpus N --steps K --warmup W]
      python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
@@ -68,6 +74,11 @@ def parse():
     ap.add_argument("--log-domain", type=int, default=LOG_PER_GPU,
                     help="log2 outputs per GPU (default 30 = the BASELINE config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-output", action="store_true",
+                    help="full_domain / full_domain_u128: also time the drop-in API call that "
+                         "returns host memory, EvaluateUntil<T>(0, {}, ctx) -> std::vector<T> "
+                         "(reported in `api_level`, never as `value`)")
+    ap.add_argument("--host-output-reps", type=int, default=3)
     ap.add_argument("--cpu-chunks", type=int, default=32,
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
     ap.add_argument("--workload", default="full_domain",
@@ -254,6 +265,51 @@ def profiled_traffic(kernel: str, leaves_per_launch: int = None):
                      "write_amplification": s.get("write_amplification"),
                      "profiled_launch_ms": s.get("avg_ns", 0) / 1e6})
     return best
+
+
+def host_output_rate(dpf, ctx0, bits: int, reps: int, dev_out, n: int, kernel_ms: float) -> dict:
+    """API-level throughput of the drop-in call the reference's callers make:
+    EvaluateUntil<T>(0, {}, ctx) -> std::vector<T> in host memory
+    (dpf/distributed_point_function.h:790-821), T = uint64_t / absl::uint128,
+    on fresh copies of the benchmark key's context (C++ timing, GIL released).
+    Its outputs are checked against the device run's at a few positions."""
+    import statistics
+    esz = bits // 8
+    probe = [0, 1, n // 3, n // 2, n - 1]
+    secs, got_n, samples = dpf._impl.time_evaluate_until(0, ctx0.SerializeToString(), bits, reps,
+                                                          probe)
+    assert got_n == n, (got_n, n)
+    dev = dev_out.view(-1)
+    for i, lo, hi in samples:
+        b = dev[i * esz:(i + 1) * esz].cpu().numpy().tobytes()
+        want = int.from_bytes(b, "little")
+        assert (lo | hi << 64) == want, ("host vs device output", i)
+    med = statistics.median(secs)
+    nbytes = n * esz
+    d2h_s = max(med - kernel_ms * 1e-3, 1e-9)
+    return {"call": f"EvaluateUntil<{'uint64_t' if bits == 64 else 'absl::uint128'}>(0, {{}}, ctx) "
+                    f"-> std::vector (host memory)",
+            "reps": reps, "api_ms_per_call": [x * 1e3 for x in secs], "api_ms_per_step": med * 1e3,
+            "api_leaves_per_s": n / med, "host_output_bytes": nbytes,
+            "host_output_gb_per_s": nbytes / med / 1e9,
+            "kernel_ms_per_step": kernel_ms,
+            "d2h_gb_per_s_beyond_kernel": nbytes / d2h_s / 1e9,
+            "note": "PCIe-inclusive; the kernel-level `value` keeps the outputs in HBM"}
+
+
+def profile_check(roof: dict, tr, aes_per_launch: float, ms_per_launch: float) -> None:
+    """Puts the committed rocprofv3 summary's timed-launch average beside this
+    run's own launch time: `frac_from_profile` is the roofline fraction the
+    summary alone gives, and `profile_slower_than_step` flags a summary whose
+    kernel is slower than this run's whole step (a profile of another box or
+    tree, not of this kernel as measured here)."""
+    if not tr or not tr[2] or not tr[2].get("profiled_launch_ms"):
+        return
+    prof_ms = tr[2]["profiled_launch_ms"]
+    roof["profiled_launch_ms"] = prof_ms
+    roof["frac_from_profile"] = aes_per_launch / (prof_ms * 1e-3) / 1e9 / roof["peak"]
+    roof["profile_vs_launch"] = prof_ms / ms_per_launch
+    roof["profile_slower_than_step"] = bool(prof_ms > ms_per_launch)
 
 
 def kernel_name(args, bits: int) -> str:
@@ -447,6 +503,10 @@ def main():
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS},
         }
+        profile_check(res["roofline"], tr, aes_per_launch, ms_per_step)
+        if args.host_output and world == 1 and args.workload in ("full_domain", "full_domain_u128"):
+            res["api_level"] = host_output_rate(dpf, ctx0, bits, args.host_output_reps, out,
+                                                outputs_per_rank, kern_ms_max)
         if world == 1 and not args.no_cpu_baseline:
             ovt = None
             if args.workload == "full_domain_tuple":

@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -132,6 +133,42 @@ class PyDpf {
     auto keys = Take(dpf_->GenerateKeysIncrementalWithSeeds(IntToU128(alpha), MakeConstSpan(v),
                                                             IntToU128(s0), IntToU128(s1)));
     return py::make_tuple(Ser(keys.first), Ser(keys.second));
+  }
+  // API-level timing of the drop-in EvaluateUntil<T>(level, {}, ctx) that
+  // returns std::vector<T> in host memory (uint64_t or absl::uint128 by
+  // `bits`): `reps` calls on fresh copies of ctx, wall seconds each (the
+  // vector's allocation, the kernel and the D2H copy included; freeing the
+  // previous vector is not).  Returns (seconds list, elements, sample of the
+  // last output: (index, low, high) at `probe` positions).
+  py::tuple TimeEvaluateUntil(int level, const py::bytes& ctx_bytes, int bits, int reps,
+                              const std::vector<int64_t>& probe) {
+    const EvaluationContext ctx0 = Parse<EvaluationContext>(ctx_bytes);
+    std::vector<double> secs;
+    int64_t n = 0;
+    std::vector<py::tuple> samples;
+    auto run = [&](auto tag) {
+      using T = decltype(tag);
+      std::vector<T> out;
+      for (int r = 0; r < reps; ++r) {
+        EvaluationContext ctx = ctx0;
+        out = std::vector<T>();  // free before the timed call
+        const auto t0 = std::chrono::steady_clock::now();
+        {
+          py::gil_scoped_release nogil;
+          out = Take(dpf_->EvaluateUntil<T>(level, {}, ctx));
+        }
+        secs.push_back(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      }
+      n = static_cast<int64_t>(out.size());
+      for (int64_t i : probe)
+        if (i >= 0 && i < n)
+          samples.push_back(py::make_tuple(i, static_cast<uint64_t>(out[i]),
+                                           static_cast<uint64_t>(uint128(out[i]) >> 64)));
+    };
+    if (bits == 64) run(uint64_t{});
+    else if (bits == 128) run(uint128{});
+    else throw StatusError(InvalidArgumentError("bits must be 64 or 128"));
+    return py::make_tuple(secs, n, samples);
   }
   py::bytes CreateEvaluationContext(const py::bytes& key) {
     return Ser(Take(dpf_->CreateEvaluationContext(Parse<DpfKey>(key))));
@@ -431,6 +468,7 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("generate_keys_incremental", &PyDpf::GenerateKeys)
       .def("generate_keys_incremental_with_seeds", &PyDpf::GenerateKeysWithSeeds)
       .def("create_evaluation_context", &PyDpf::CreateEvaluationContext)
+      .def("time_evaluate_until", &PyDpf::TimeEvaluateUntil)
       .def("evaluate_until", &PyDpf::EvaluateUntil)
       .def("evaluate_until_to_device", &PyDpf::EvaluateUntilToDevice)
       .def("evaluate_shard_to_device", &PyDpf::EvaluateShardToDevice)

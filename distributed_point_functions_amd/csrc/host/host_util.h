@@ -346,7 +346,10 @@ class PackedUploads {
 
 // Orders reuse of a device buffer across calls that may come on different
 // streams: Mark(stream) records an event after the last kernel that touches
-// the buffer; Wait() blocks on it before the next call rewrites the buffer.
+// the buffer; Acquire(buf, bytes, stream) makes the next call's work wait for
+// it -- on the device (hipStreamWaitEvent) when the stream differs, not at
+// all on the same stream (stream order), and on the host only when the
+// buffer must be reallocated (freeing memory a kernel may still use).
 class StreamFence {
  public:
   StreamFence() = default;
@@ -356,21 +359,29 @@ class StreamFence {
     if (pending_) (void)dpf_hip_event_sync(event_);
     if (event_) dpf_hip_event_destroy(event_);
   }
-  Status Wait() {
-    if (pending_) HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
-    pending_ = false;
-    return OkStatus();
+  Status Acquire(DeviceBuffer& buf, size_t bytes, void* stream) {
+    if (pending_) {
+      if (bytes > buf.capacity() || !buf.get()) {
+        HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
+        pending_ = false;
+      } else if (stream != last_stream_) {
+        HIP_RETURN_IF_ERROR(dpf_hip_stream_wait_event(stream, event_));
+      }
+    }
+    return buf.Reserve(bytes);
   }
   Status Mark(void* stream) {
     if (!event_) HIP_RETURN_IF_ERROR(dpf_hip_event_create(&event_));
     HIP_RETURN_IF_ERROR(dpf_hip_event_record(event_, stream));
     pending_ = true;
+    last_stream_ = stream;
     return OkStatus();
   }
 
  private:
   bool pending_ = false;
   void* event_ = nullptr;
+  void* last_stream_ = nullptr;
 };
 
 class DeviceScratch {

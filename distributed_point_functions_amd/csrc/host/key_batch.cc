@@ -383,9 +383,9 @@ Status DistributedPointFunction::EvaluateAtBatchSumToDevice(const DeviceKeyBatch
                                        std::to_string(hierarchy_level));
   auto* s = scratch_.get();
   // The workspace is zeroed and accumulated into on `stream`: an earlier call
-  // on another stream must have finished with it first.
-  DPF_RETURN_IF_ERROR(s->workspace_fence.Wait());
-  DPF_RETURN_IF_ERROR(s->workspace.Reserve(num_points * f.leaves.size() * 3 * sizeof(uint64_t)));
+  // on another stream must have finished with it first (device-side wait).
+  DPF_RETURN_IF_ERROR(s->workspace_fence.Acquire(
+      s->workspace, num_points * f.leaves.size() * 3 * sizeof(uint64_t), stream));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   HIP_RETURN_IF_ERROR(dpf_hip_eval_points_sum(

@@ -144,16 +144,16 @@ StatusOr<bool> ValueTypesAreEqual(const ValueType& lhs, const ValueType& rhs) {
   return false;
 }
 
-double IntModNSecurityLevel(int num_samples, uint128 modulus) {
+double IntModNBase::GetSecurityLevel(int num_samples, uint128 modulus) {
   // int_mod_n.cc:21-26
   return 128 + 3 -
          (std::log2(static_cast<double>(modulus)) + std::log2(static_cast<double>(num_samples)) +
           std::log2(static_cast<double>(num_samples + 1)));
 }
 
-Status IntModNCheckParameters(int num_samples, int base_integer_bitsize, uint128 modulus,
-                              double security_parameter) {
-  // int_mod_n.cc:28-65
+Status IntModNBase::CheckParameters(int num_samples, int base_integer_bitsize, uint128 modulus,
+                                    double security_parameter) {
+  // int_mod_n.cc:28-61
   if (num_samples <= 0) return InvalidArgumentError("num_samples must be positive");
   if (base_integer_bitsize <= 0) return InvalidArgumentError("base_integer_bitsize must be positive");
   if (base_integer_bitsize > 128)
@@ -162,7 +162,7 @@ Status IntModNCheckParameters(int num_samples, int base_integer_bitsize, uint128
     return InvalidArgumentError("kModulus " + Uint128ToString(modulus) +
                                 " out of range for base_integer_bitsize = " +
                                 std::to_string(base_integer_bitsize));
-  const double sigma = IntModNSecurityLevel(num_samples, modulus);
+  const double sigma = GetSecurityLevel(num_samples, modulus);
   if (security_parameter > sigma) {
     char buf[64];
     snprintf(buf, sizeof(buf), "%f", sigma);
@@ -175,11 +175,11 @@ Status IntModNCheckParameters(int num_samples, int base_integer_bitsize, uint128
   return OkStatus();
 }
 
-StatusOr<int> IntModNNumBytesRequired(int num_samples, int base_integer_bitsize, uint128 modulus,
-                                      double security_parameter) {
-  // int_mod_n.cc:67-78
+StatusOr<int> IntModNBase::GetNumBytesRequired(int num_samples, int base_integer_bitsize,
+                                               uint128 modulus, double security_parameter) {
+  // int_mod_n.cc:63-76
   DPF_RETURN_IF_ERROR(
-      IntModNCheckParameters(num_samples, base_integer_bitsize, modulus, security_parameter));
+      CheckParameters(num_samples, base_integer_bitsize, modulus, security_parameter));
   return 16 + ((base_integer_bitsize + 7) / 8) * (num_samples - 1);
 }
 

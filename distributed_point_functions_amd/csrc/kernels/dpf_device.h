@@ -47,19 +47,11 @@ constexpr int kWgPerCu = 1;              // one 128 KiB-table workgroup per CU
 constexpr int kTabWords = 4 * 256 * 32;  // 4 tables x 256 entries x 32 bank copies = 128 KiB
 #define DPF_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(4, 4)))
 constexpr int kMaxCwLevels = 128;
-#if defined(DPF_LEAF_QUADS)
-#ifndef DPF_QUAD_SMAX
-#define DPF_QUAD_SMAX 11
-#endif
-constexpr int kSMax = DPF_QUAD_SMAX;     // max subtree depth handled per thread
-constexpr int kGMax = kSMax - 2;         // max depth of the DFS stack above leaf quads
-#else
 #ifndef DPF_SMAX
 #define DPF_SMAX 12
 #endif
 constexpr int kSMax = DPF_SMAX;          // max subtree depth handled per thread
 constexpr int kGMax = kSMax - 1;         // max depth of the DFS stack above leaf pairs
-#endif
 constexpr int kBMax = 8;                 // max AES blocks hashed per leaf (generic path)
 
 // LDS image: [tables 128 KiB][cw seeds 128 x 16 B][cw control 128 x 4 B]

@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <type_traits>
 #include <thread>
 #include <vector>
 #include <string>
@@ -35,6 +36,8 @@
 
 namespace dpf_rt {
 thread_local std::string g_last_error;
+thread_local const char* g_last_expand = "";
+thread_local int g_last_expand_s = -1;
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -111,13 +114,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
   __syncthreads();
   const LdsLookup lk = make_lookup(lds);
   const int k0 = p.k0, S = p.S;
-#if defined(DPF_LEAF_QUADS)
-  // Bottom two levels as quads: a grandparent's two children, their four
-  // children and the four value hashes, the last eight AES as ILP4.
-  const int B = S >= 2 ? 2 : (S >= 1 ? 1 : 0);
-#else
   const int B = S >= 1 ? 1 : 0;  // leaf pairs share their parent
-#endif
   const int G = S - B;            // depth of the DFS stack
   const int64_t ngroups = (int64_t)1 << G;
   for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
@@ -161,32 +158,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
       }
       if (B == 0) {
         leaf.emit(lk, p.rkv.k, node, nt, leaf_base + g, p.out);
-#if defined(DPF_LEAF_QUADS)
-      } else if (B == 2) {
-        const int lvl = k0 + G;
-        Block4 q[4];
-        uint32_t qt[4];
-        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], q[0],
-                      qt[0], q[2], qt[2]);
-        q[1] = q[0];
-        q[3] = q[2];
-        {
-          const UniformRK rk[4] = {UniformRK{p.rkl.k}, UniformRK{p.rkr.k}, UniformRK{p.rkl.k},
-                                   UniformRK{p.rkr.k}};
-          dpf_aes::mmo_hashN<4>(q, lk, rk);
-          const uint4 cs = lds.cw_seed[lvl + 1];
-          const uint32_t cctl = lds.cw_ctrl[lvl + 1];
-          const uint32_t par[4] = {qt[0], qt[0], qt[2], qt[2]};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t m = 0u - par[i];
-            q[i].w0 ^= cs.x & m; q[i].w1 ^= cs.y & m; q[i].w2 ^= cs.z & m; q[i].w3 ^= cs.w & m;
-            qt[i] = (q[i].w0 & 1u) ^ (par[i] & ((cctl >> (i & 1)) & 1u));
-            q[i].w0 &= ~1u;
-          }
-        }
-        leaf.emit4(lk, p.rkv.k, q, qt, leaf_base + 4 * g, p.out);
-#endif
       } else {
         const int lvl = k0 + G;
         Block4 c0, c1;
@@ -504,125 +475,6 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(Poin
   }
 }
 
-// Four path walks per lane (ILP4) for integer / XorWrapper leaves: item u
-// covers points (q, q + part, q + 2 part, q + 3 part) of its key (or key
-// chunk in sum mode), part = ceil(P / 4); otherwise as eval_points_kernel.
-// Opt-in (DPF_POINTS_QUAD=1) for per-key (non-sum) launches: 112-122 VGPRs
-// cost more occupancy than the extra ILP buys; a sum form would spill.
-template <int N>
-__device__ __forceinline__ void path_stepN(const LdsLookup& lk, const RoundKeys& rkl,
-                                           const RoundKeys& rkd, Block4* s, uint32_t* t,
-                                           const uint32_t* b, uint4 cs, uint32_t cctl) {
-  Block4 h[N];
-  SelectRK rk[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    h[i] = s[i];
-    rk[i] = SelectRK{rkl.k, rkd.k, 0u - b[i]};
-  }
-  dpf_aes::mmo_hashN<N>(h, lk, rk);
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const uint32_t m = 0u - t[i];
-    h[i].w0 ^= cs.x & m; h[i].w1 ^= cs.y & m; h[i].w2 ^= cs.z & m; h[i].w3 ^= cs.w & m;
-    const uint32_t n = (h[i].w0 & 1u) ^ (t[i] & ((cctl >> b[i]) & 1u));
-    h[i].w0 &= ~1u;
-    s[i] = h[i];
-    t[i] = n;
-  }
-}
-
-template <int BITS, bool UNIFORM, bool SUM>
-__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(PointParams p) {
-  __shared__ LdsImage lds;
-  fill_tables(lds.tab);
-  __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
-  const int L = p.num_levels;
-  const int64_t P = p.points_per_key, part = p.half;
-  const UniformRK rv[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
-                           UniformRK{p.rkv.k}};
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
-       u += (int64_t)gridDim.x * blockDim.x) {
-    int64_t grp = u / part;
-    if (UNIFORM) grp = (int64_t)__builtin_amdgcn_readfirstlane((int)grp);
-    const int64_t q0 = u - grp * part;
-    int64_t q[4];
-    bool has[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t qr = q0 + j * part;
-      has[j] = qr < P;
-      q[j] = has[j] ? qr : q0;
-    }
-    int64_t k_begin = grp, k_end = grp + 1;
-    if (SUM) {
-      k_begin = grp * p.chunk_keys;
-      k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
-    }
-    Block4 path[4];
-    int bi[4];
-    const int bb = p.bib;
-    const uint32_t bmask = (1u << bb) - 1u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t pi = p.shared_points ? q[j] : grp * P + q[j];
-      path[j] = load_block(p.tree_index + pi);
-      bi[j] = p.block_index ? p.block_index[pi] : (int)(path[j].w0 & bmask);
-    }
-    u128 acc[4] = {0, 0, 0, 0};
-    for (int64_t k = k_begin; k < k_end; ++k) {
-      const int party = p.party[k] & 1;
-      Block4 st[4];
-      uint32_t t[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (p.seeds_in) {
-          const int64_t o = k * P + q[j];
-          st[j] = load_block(p.seeds_in + o);
-          t[j] = p.ctrl_in[o] & 1u;
-        } else {
-          st[j] = load_block(p.key_seed + k);
-          t[j] = (uint32_t)party;
-        }
-      }
-      const dpf_block* cws = p.cw_seed + k * p.cw_stride;
-      const uint8_t* cl = p.cw_left + k * p.cw_stride;
-      const uint8_t* cr = p.cw_right + k * p.cw_stride;
-      for (int lv = 0; lv < L; ++lv) {
-        uint32_t b[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = path_bit(path[j], L - 1 - lv + bb);
-        const dpf_block c = cws[lv];
-        const uint32_t cctl = (uint32_t)(cl[lv] & 1) | ((uint32_t)(cr[lv] & 1) << 1);
-        const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
-                                    (uint32_t)(c.high >> 32));
-        path_stepN<4>(lk, p.rkl, p.rkd, st, t, b, cs, cctl);
-      }
-      dpf_aes::mmo_hashN<4>(st, lk, rv);
-      const dpf_block* vcw = p.vcw + k * p.vcw_stride;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const u128 v = fast_point_value<BITS>(st[j], t[j], bi[j], dpf_u128(vcw[bi[j]]), party,
-                                              p.xor_mode);
-        if (SUM) {
-          acc[j] = p.xor_mode ? (acc[j] ^ v) : (acc[j] + v);
-        } else if (has[j]) {
-          store_bits<BITS>(p.out + (k * P + q[j]) * (int64_t)p.esz, v);
-        }
-      }
-    }
-    if (SUM && k_begin < k_end) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (!has[j]) continue;
-        unsigned long long* w = p.wide + q[j] * 3;
-        if (p.xor_mode) wide_xor(w, acc[j]); else wide_add(w, acc[j]);
-      }
-    }
-  }
-}
-
 // Counts points >= 2^log_domain_size (EvaluateAt's range check, h:861-874).
 __global__ void count_out_of_range_kernel(int64_t n, const dpf_block* __restrict__ pts, int log,
                                           unsigned long long* __restrict__ bad) {
@@ -744,7 +596,26 @@ bool fast_int(const dpf_value_desc* d) {
 namespace {
 
 template <class Leaf>
+const char* leaf_name() {
+  if constexpr (std::is_same_v<Leaf, SwarLeaf>) return "swar";
+  else if constexpr (std::is_same_v<Leaf, GenericLeaf>) return "generic";
+  else if constexpr (std::is_same_v<Leaf, Mod32Leaf<2>> ||
+                     std::is_same_v<Leaf, Mod32Leaf<kMod32MaxLeaves>>) return "mod32";
+  else return "fast";
+}
+
+// Records the launch for dpf_hip_last_expand_kernel().
+template <class Leaf>
+void note_expand(const ExpandParams& p, bool octet) {
+  static const std::string pair = std::string("pair/") + leaf_name<Leaf>();
+  static const std::string oct = std::string("octet/") + leaf_name<Leaf>();
+  g_last_expand = octet ? oct.c_str() : pair.c_str();
+  g_last_expand_s = p.S;
+}
+
+template <class Leaf>
 int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
+  note_expand<Leaf>(p, false);
   const int blk = block_for(p.num_items);
   hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid_for(p.num_items, blk)), dim3(blk), 0, s, p,
                      leaf);
@@ -759,6 +630,7 @@ bool launch_octet(const ExpandParams& p, const dpf_block* vcw, int E, int party,
                   hipStream_t s) {
   const char* off = getenv("DPF_EXPAND_NO_OCTET");
   if ((off && off[0] == '1') || store_bytes != 16 || p.S < 3) return false;
+  note_expand<FastIntLeaf<BITS, XOR>>(p, true);
   const int blk = block_for(p.num_items);
   hipLaunchKernelGGL((expand_octet_kernel<FastIntLeaf<BITS, XOR>>), dim3(grid_for(p.num_items, blk)),
                      dim3(blk), 0, s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
@@ -794,26 +666,6 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
       else
         hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, false, false, false>), grid,
                            block, 0, s, p, leaf);
-      HIP_TRY(hipGetLastError());
-      return kOk;
-    }
-  }
-  if constexpr (FAST && !SUM) {
-    // Quads (ILP4) only on request (DPF_POINTS_QUAD=1): at config 4 they
-    // measured 674 M points/s against the pairs' 726 M.
-    const char* env = getenv("DPF_POINTS_QUAD");
-    const int64_t groups = pp.num_items / pp.half;
-    const int64_t part = (pp.points_per_key + 3) / 4;
-    if (env && env[0] == '1') {
-      PointParams p = pp;
-      p.half = part;
-      p.num_items = groups * part;
-      const int blk = block_for(p.num_items);
-      const dim3 grid(grid_for(p.num_items, blk)), block(blk);
-      if (part % 64 == 0)
-        hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM>), grid, block, 0, s, p);
-      else
-        hipLaunchKernelGGL((eval_points4_kernel<BITS, false, SUM>), grid, block, 0, s, p);
       HIP_TRY(hipGetLastError());
       return kOk;
     }
@@ -901,6 +753,11 @@ extern "C" {
 
 int dpf_hip_abi_version(void) { return DPF_HIP_ABI_VERSION; }
 const char* dpf_hip_last_error(void) { return dpf_rt::g_last_error.c_str(); }
+
+const char* dpf_hip_last_expand_kernel(int* subtree_depth) {
+  if (subtree_depth) *subtree_depth = dpf_rt::g_last_expand_s;
+  return dpf_rt::g_last_expand;
+}
 
 int dpf_hip_device_count(int* count) {
   HIP_TRY(hipGetDeviceCount(count));
@@ -1055,6 +912,10 @@ int dpf_hip_event_sync(void* event) {
   HIP_TRY(hipEventSynchronize((hipEvent_t)event));
   return kOk;
 }
+int dpf_hip_stream_wait_event(void* stream, void* event) {
+  HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+  return kOk;
+}
 int dpf_hip_packed_element_size(const dpf_value_desc* desc) {
   if (!desc) return -1;
   return packed_size(desc);
@@ -1129,38 +990,6 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
     return fail(kInvalidArgument, "NULL pointer");
   if (num_starts > (INT64_MAX >> num_levels))
     return fail(kInvalidArgument, "expansion too large");
-  if (expand_hybrid_applies(num_starts, num_levels, key_value, desc, elements_per_leaf))
-    return launch_expand_hybrid(num_starts, seeds_in, control_in, num_levels, cw_seed, cw_left,
-                                cw_right, key_left, key_right, key_value, desc, value_correction,
-                                party, out, (hipStream_t)stream);
-  // Integer leaves filling whole blocks: the wave-specialised kernel when it is
-  // enabled (DPF_EXPAND_WS=1, opt-in) and the tree gives every tree lane a
-  // subtree (dpf_expand_ws.hip).
-  {
-    int bits = 0, lanes = 0, sb = 0, kind = 0;
-    if (fast_int(desc)) {
-      bits = desc->bits[0];
-      lanes = desc->elements_per_block;
-      sb = elements_per_leaf * bits / 8;
-      kind = desc->kind[0];
-    } else if (desc->direct && desc->blocks_needed == 1) {
-      bool uniform = true;
-      for (int k = 1; k < desc->num_leaves; ++k)
-        uniform = uniform && desc->bits[k] == desc->bits[0] && desc->kind[k] == desc->kind[0];
-      if (uniform && desc->kind[0] != DPF_LEAF_INTMODN &&
-          desc->elements_per_block * desc->num_leaves * desc->bits[0] <= 128) {
-        bits = desc->bits[0];
-        lanes = desc->elements_per_block * desc->num_leaves;
-        sb = elements_per_leaf * packed_size(desc);
-        kind = desc->kind[0];
-      }
-    }
-    if (sb == 16 && expand_ws_applies(num_starts, num_levels, key_value))
-      return launch_expand_ws(num_starts, seeds_in, control_in, num_levels, cw_seed, cw_left,
-                              cw_right, key_left, key_right, key_value, bits,
-                              kind == DPF_LEAF_XOR, lanes, value_correction, party, out,
-                              (hipStream_t)stream);
-  }
   // Choose the depth-first subtree depth S (items = num_starts * 2^(L - S)
   // subtrees, each walked k0 = L - S levels from its start seed) by the
   // per-thread critical path: rounds of items over the launch's threads times
@@ -1254,6 +1083,7 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       }
       const char* off_env = getenv("DPF_EXPAND_NO_OCTET");
       if (p.S >= 3 && !(off_env && off_env[0] == '1')) {
+        note_expand<SwarLeaf>(p, true);
         const int blk = block_for(p.num_items);
         hipLaunchKernelGGL((expand_octet_kernel<SwarLeaf>), dim3(grid_for(p.num_items, blk)),
                            dim3(blk), 0, s, p, w);
@@ -1280,6 +1110,7 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       const char* off = getenv("DPF_EXPAND_NO_OCTET");
       if (p.S >= 3 && !(off && off[0] == '1')) {
         // Octet form (the half's four leaves hashed as two ILP4 groups).
+        note_expand<Mod32Leaf<2>>(p, true);
         const int blk = block_for(p.num_items);
         hipLaunchKernelGGL((expand_octet_kernel<Mod32Leaf<2>>), dim3(grid_for(p.num_items, blk)),
                            dim3(blk), 0, s, p, m);

@@ -26,30 +26,6 @@ int validate_desc(const dpf_value_desc* d);    // kOk or the failure code
 int packed_size(const dpf_value_desc* d);      // bytes of one packed element
 bool fast_int(const dpf_value_desc* d);        // one plain/XOR integer leaf, direct, b == 1
 
-// dpf_expand_hybrid.hip: full-domain expansion with the leaf value hashes
-// bitsliced on the VALU beside the LDS T-table (plain/XOR integer leaves,
-// whole blocks, the reference's value key, at least 8 leaves per lane).
-bool expand_hybrid_applies(int64_t num_starts, int num_levels, const dpf_aes_key* key_value,
-                           const dpf_value_desc* desc, int elements_per_leaf);
-int launch_expand_hybrid(int64_t num_starts, const dpf_block* seeds_in, const uint8_t* control_in,
-                         int num_levels, const dpf_block* cw_seed, const uint8_t* cw_left,
-                         const uint8_t* cw_right, const dpf_aes_key* key_left,
-                         const dpf_aes_key* key_right, const dpf_aes_key* key_value,
-                         const dpf_value_desc* desc, const dpf_block* value_correction, int party,
-                         void* out, hipStream_t s);
-
-// dpf_expand_ws.hip: full-domain expansion in wave-specialised workgroups (12
-// T-table tree waves + 4 bitsliced value waves per CU) for integer leaves that
-// fill whole 16-byte blocks, the reference's value key, and at least one
-// subtree of depth >= 5 per tree lane.
-bool expand_ws_applies(int64_t num_starts, int num_levels, const dpf_aes_key* key_value);
-int launch_expand_ws(int64_t num_starts, const dpf_block* seeds_in, const uint8_t* control_in,
-                     int num_levels, const dpf_block* cw_seed, const uint8_t* cw_left,
-                     const uint8_t* cw_right, const dpf_aes_key* key_left,
-                     const dpf_aes_key* key_right, const dpf_aes_key* key_value, int bits,
-                     bool xor_leaf, int elements, const dpf_block* value_correction, int party,
-                     void* out, hipStream_t s);
-
 }  // namespace dpf_rt
 
 #define HIP_TRY(expr)                                           \

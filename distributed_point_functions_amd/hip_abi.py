@@ -74,6 +74,8 @@ def load(require_gpu: bool = False):
         L = ctypes.CDLL(LIB_PATH)
         P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
         L.dpf_hip_last_error.restype = ctypes.c_char_p
+        L.dpf_hip_last_expand_kernel.restype = ctypes.c_char_p
+        L.dpf_hip_last_expand_kernel.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.dpf_hip_hash.argtypes = [I64, P, P, P, P]
         L.dpf_hip_eval_paths.argtypes = [I64, I, P, P, P, P, P, P, P, P, P, P, P]
         L.dpf_hip_expand.argtypes = [I64, P, P, I, P, P, P, P, P, P, P, I, P, I, P, P]
@@ -93,6 +95,14 @@ def load(require_gpu: bool = False):
         if not torch.cuda.is_available():
             raise DpfHipError(13, "no GPU visible: the DPF engine has no CPU fallback")
     return _lib
+
+
+def last_expand_kernel():
+    """(kernel, subtree depth) of this thread's last dpf_hip_expand launch,
+    e.g. ("octet/mod32", 3) -- dispatch diagnostics for the tests."""
+    d = ctypes.c_int(-1)
+    name = load().dpf_hip_last_expand_kernel(ctypes.byref(d)).decode()
+    return name, d.value
 
 
 def check(st: int):

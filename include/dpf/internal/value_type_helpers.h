@@ -52,12 +52,20 @@ StatusOr<uint128> ValueIntegerToUint128(const Value::Integer& in);
 Value::Integer Uint128ToValueInteger(uint128 in);
 std::string SerializeValueTypeDeterministically(const ValueType& value_type);
 
-// IntModNBase (dpf/int_mod_n.cc).
-double IntModNSecurityLevel(int num_samples, uint128 modulus);
-Status IntModNCheckParameters(int num_samples, int base_integer_bitsize, uint128 modulus,
-                              double security_parameter);
-StatusOr<int> IntModNNumBytesRequired(int num_samples, int base_integer_bitsize, uint128 modulus,
-                                      double security_parameter);
+// Shorthands for IntModNBase (dpf/int_mod_n.h, int_mod_n.cc).
+inline double IntModNSecurityLevel(int num_samples, uint128 modulus) {
+  return IntModNBase::GetSecurityLevel(num_samples, modulus);
+}
+inline Status IntModNCheckParameters(int num_samples, int base_integer_bitsize, uint128 modulus,
+                                     double security_parameter) {
+  return IntModNBase::CheckParameters(num_samples, base_integer_bitsize, modulus,
+                                      security_parameter);
+}
+inline StatusOr<int> IntModNNumBytesRequired(int num_samples, int base_integer_bitsize,
+                                             uint128 modulus, double security_parameter) {
+  return IntModNBase::GetNumBytesRequired(num_samples, base_integer_bitsize, modulus,
+                                          security_parameter);
+}
 
 // FromValue for a runtime ValueType, with the reference's error messages.
 StatusOr<std::vector<uint128>> ValueToLeaves(const ValueType& type, const Value& value);

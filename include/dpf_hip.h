@@ -98,6 +98,8 @@ int dpf_hip_stream_sync(void* stream);
  * staging buffers with one, so reusing them never depends on the caller's
  * stream still existing. */
 int dpf_hip_event_sync(void* event);
+/* Makes later work on `stream` wait for `event` on the device (no host wait). */
+int dpf_hip_stream_wait_event(void* stream, void* event);
 /* Packed size in bytes of one output element: sum of leaf bits / 8. */
 int dpf_hip_packed_element_size(const dpf_value_desc* desc);
 
@@ -137,6 +139,12 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
                    const dpf_aes_key* key_right, const dpf_aes_key* key_value,
                    const dpf_value_desc* desc, int elements_per_leaf,
                    const dpf_block* value_correction, int party, void* out, void* stream);
+
+/* Diagnostic: which kernel the calling thread's last successful dpf_hip_expand
+ * launched ("octet/<leaf>" or "pair/<leaf>", leaf = fast, swar, mod32,
+ * generic; "" before the first call), and the depth-first subtree depth it
+ * chose.  Tests use it to pin the dispatch. */
+const char* dpf_hip_last_expand_kernel(int* subtree_depth);
 
 /* ---- a11: fused point evaluation for many keys ----------------------------
  * Replaces EvaluateAtImpl's path walk + hash + correction (h:930-1003).

@@ -1,4 +1,4 @@
-// Host checks of the bitsliced AES engine (csrc/kernels/bs_aes.h) against the
+// Host checks of the bitsliced AES engine (tools/bs_aes.h) against the
 // FIPS-197 S-box and the T-table MMO hash of aes_core.h (itself pinned by the
 // reference KAT, tests/test_oracle.py).  Built and run by tests/test_bs_aes_cpu.py.
 #include <stdio.h>
@@ -7,7 +7,7 @@
 #include <random>
 
 #include "../../distributed_point_functions_amd/csrc/kernels/aes_core.h"
-#include "../../distributed_point_functions_amd/csrc/kernels/bs_aes.h"
+#include "../../tools/bs_aes.h"
 
 static int g_bad = 0;
 

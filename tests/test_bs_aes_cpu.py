@@ -1,4 +1,4 @@
-"""Host checks of the bitsliced AES engine (csrc/kernels/bs_aes.h, the VALU
+"""Host checks of the bitsliced AES engine (tools/bs_aes.h, the VALU
 half of the hybrid expand kernel): the 82-gate bitop3 S-box on all 256 inputs,
 the plane transposes, the MMO hash with run-time and compile-time key masks
 against the T-table AES of aes_core.h (pinned by the reference KAT in

@@ -181,18 +181,32 @@ def test_expand_specialised_leaves(hip, vt, party, sec):
     _expand_case(hip, rng, vt, 3, 17, party, sec=sec)
 
 
-# The opt-in hybrid kernel (DPF_EXPAND_HYBRID=1), shapes above its threshold (>= 8 leaves per lane of a full
-# launch, dpf_expand_hybrid.hip): the leaf value hashes run bitsliced on the
-# VALU, the inner nodes on the T-table; (3, 2^18) is octets only (S = 3).
-@pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
-@pytest.mark.parametrize("levels,n0", [(21, 1), (18, 9), (3, 1 << 18)])
+# The same types at octet-sized shapes: subtrees of >= 8 leaves per lane, so
+# dpf_hip_expand dispatches expand_octet_kernel<Leaf> (FastIntLeaf lanes,
+# SwarLeaf, Mod32Leaf<2>); both that launch and the pair kernel
+# (DPF_EXPAND_NO_OCTET=1) must match the oracle, and the dispatch is checked.
+# Expected launch per type: Tuple<uint16_t x3> stores 12-byte leaves and 3 or
+# 4 IntModN32 leaves use Mod32Leaf<4>, both on the pair kernel.
+EXPECTED_KERNEL = ["octet/fast", "pair/fast", "octet/swar", "octet/swar", "octet/swar",
+                   "octet/swar", "octet/swar", "octet/mod32", "octet/mod32", "pair/mod32",
+                   "octet/mod32", "pair/mod32"]
+
+
+@pytest.mark.parametrize("i", range(len(SPECIALISED_TYPES)),
+                         ids=[str(v) for v in SPECIALISED_TYPES])
 @pytest.mark.parametrize("party", [0, 1])
-def test_expand_hybrid_shapes(hip, vt, levels, n0, party, monkeypatch):
-    if (levels, n0) != (21, 1) and vt not in (("int", 64), ("xor", 128), ("int", 8)):
-        pytest.skip("shape covered by the other types")
-    monkeypatch.setenv("DPF_EXPAND_HYBRID", "1")   # opt-in kernel
-    rng = np.random.default_rng(hash((str(vt), levels, n0, party, "hyb")) & 0xFFFFFFFF)
-    _expand_case(hip, rng, vt, n0, levels, party)
+@pytest.mark.parametrize("levels,n0", [(21, 1), (18, 5)])
+def test_expand_specialised_leaves_octet(hip, i, party, levels, n0, monkeypatch):
+    vt = SPECIALISED_TYPES[i]
+    seed = hash((str(vt), party, levels, n0, "octet")) & 0xFFFFFFFF
+    _expand_case(hip, np.random.default_rng(seed), vt, n0, levels, party, sec=40.0)
+    name, depth = hip.last_expand_kernel()
+    want = EXPECTED_KERNEL[i]
+    assert name == want and depth >= 3, (name, depth)
+    if want.startswith("octet/"):
+        monkeypatch.setenv("DPF_EXPAND_NO_OCTET", "1")
+        _expand_case(hip, np.random.default_rng(seed), vt, n0, levels, party, sec=40.0)
+        assert hip.last_expand_kernel()[0] == "pair/" + want[6:]
 
 
 # Start counts that are not powers of two: dpf_hip_expand picks the subtree
@@ -204,52 +218,6 @@ def test_expand_hybrid_shapes(hip, vt, levels, n0, party, monkeypatch):
 def test_expand_uneven_starts(hip, vt, levels, n0, party):
     rng = np.random.default_rng(hash((str(vt), levels, n0, party, "uneven")) & 0xFFFFFFFF)
     _expand_case(hip, rng, vt, n0, levels, party)
-
-
-# The opt-in wave-specialised kernel (DPF_EXPAND_WS=1, dpf_expand_ws.hip) for
-# integer leaves filling whole blocks once every tree lane of a full launch
-# (256 CUs x 768) gets a subtree of depth >= 5: 12 T-table waves per CU expand
-# the tree and hand half-octets of leaf seeds through LDS slots to 4 bitsliced
-# waves.
-# Shapes: (23, 1) runs rounds at depths 5, 3, 3; (24, 3) exactly one round;
-# (22, 7) a last round of 2^17 lanes; (6, 196645) a last round whose final
-# wave is partly idle (148 subtrees of depth 4).
-WS_SHAPES = [(23, 1), (24, 3), (22, 7), (6, 196645)]
-
-
-@pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
-@pytest.mark.parametrize("levels,n0", WS_SHAPES)
-@pytest.mark.parametrize("party", [0, 1])
-def test_expand_ws_shapes(hip, vt, levels, n0, party, monkeypatch):
-    if (levels, n0) != (23, 1) and vt not in (("int", 64), ("xor", 128), ("int", 8)):
-        pytest.skip("shape covered by the other types")
-    monkeypatch.setenv("DPF_EXPAND_WS", "1")
-    rng = np.random.default_rng(hash((str(vt), levels, n0, party, "ws")) & 0xFFFFFFFF)
-    _expand_case(hip, rng, vt, n0, levels, party)
-
-
-@pytest.mark.parametrize("levels,n0", [(23, 1), (6, 196645)])
-def test_expand_ws_matches_octet_kernel(hip, levels, n0, monkeypatch):
-    # Same inputs through the wave-specialised and the octet kernel.
-    import torch
-    vt = ("int", 64)
-    rng = np.random.default_rng(levels * 1000 + n0)
-    seeds = _rand_blocks(rng, n0)
-    ctrl = rng.integers(0, 2, size=n0, dtype=np.uint8)
-    cws = _rand_blocks(rng, levels)
-    cl = rng.integers(0, 2, size=levels, dtype=np.uint8)
-    cr = rng.integers(0, 2, size=levels, dtype=np.uint8)
-    vcw = [_rand_value(rng, vt) for _ in range(2)]
-    args = (hip.to_device_blocks(seeds), hip.to_device_u8(ctrl), hip.to_device_blocks(cws),
-            hip.to_device_u8(cl), hip.to_device_u8(cr),
-            (O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE), _desc(hip, vt, 1), 2,
-            hip.to_device_blocks(O._leaf_array(vcw)), 1)
-    monkeypatch.setenv("DPF_EXPAND_WS", "1")
-    ws = hip.expand(*args)
-    monkeypatch.setenv("DPF_EXPAND_WS", "0")
-    octet = hip.expand(*args)
-    torch.cuda.synchronize()
-    assert torch.equal(ws, octet)
 
 
 @pytest.mark.parametrize("vt,cepb", [(("int", 8), 1), (("int", 8), 4), (("int", 16), 2),
@@ -330,15 +298,14 @@ def test_eval_points_pairing_threshold(hip, vt, ppk):
     _points_case(hip, np.random.default_rng(ppk), vt, 1, ppk, 20)
 
 
-# The quad (four chains per lane) point kernel, forced on at small sizes:
-# ragged P (P % 4 != 0, P < 4), wave-uniform parts (P = 256, 1024) and partials.
+# Ragged and wave-uniform point counts (P % 4 != 0, P < 4, P = 256, 1024),
+# with and without partial-evaluation starts.
 @pytest.mark.parametrize("vt,num_keys,ppk,levels,partials", [
     (("int", 64), 1, 777, 20, False), (("int", 64), 37, 64, 63, False),
     (("int", 64), 9, 256, 1, False), (("int", 32), 3, 1024, 30, False),
     (("int", 128), 5, 6, 127, False), (("xor", 128), 5, 100, 12, True),
     (("int", 8), 4, 5, 0, False), (("int", 16), 2, 3, 9, False),
     (("xor", 64), 11, 13, 40, True)], ids=str)
-def test_eval_points_quad(hip, monkeypatch, vt, num_keys, ppk, levels, partials):
-    monkeypatch.setenv("DPF_POINTS_QUAD", "1")
+def test_eval_points_shapes(hip, vt, num_keys, ppk, levels, partials):
     _points_case(hip, np.random.default_rng(ppk * 31 + levels), vt, num_keys, ppk, levels,
                  from_partials=partials)

@@ -1,5 +1,5 @@
 // bs_microbench.hip -- throughput of the bitsliced MMO hash of
-// csrc/kernels/bs_aes.h on one MI355X (VALU only, no LDS): 8 blocks per lane,
+// tools/bs_aes.h on one MI355X (VALU only, no LDS): 8 blocks per lane,
 // normal form in and out (transposes included), key masks from the kernel
 // arguments.  Also checks the GPU result against the T-table hash on the host.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/bs_microbench.hip -o /tmp/bsmb
@@ -11,7 +11,7 @@
 #include <vector>
 
 #include "../distributed_point_functions_amd/csrc/kernels/aes_core.h"
-#include "../distributed_point_functions_amd/csrc/kernels/bs_aes.h"
+#include "bs_aes.h"
 
 #ifndef BS_WAVES
 #define BS_WAVES 4

@@ -1,5 +1,5 @@
 """Maps the Boyar-Peralta AES S-box circuit onto gfx950 3-input LUT gates
-(v_bitop3_b32) and emits the C++ body used by csrc/kernels/bs_aes.h.
+(v_bitop3_b32) and emits the C++ body used by tools/bs_aes.h.
 
 The BP circuit ("A depth-16 circuit for the AES S-box", Boyar and Peralta 2011:
 32 AND, 77 XOR, 4 XNOR) is covered with 3-feasible cuts; an exact ILP

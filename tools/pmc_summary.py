@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--total", action="store_true",
                     help="sum every matching dispatch (a workload of many differently sized "
                          "launches, e.g. one heavy-hitters pass): --aes/--bytes are totals")
+    ap.add_argument("--skip", type=int, default=0,
+                    help="per-launch mode: drop the first N launches (bench.py's --warmup "
+                         "steps) so avg_ns is the bench's timed region")
     ap.add_argument("--leaves", type=int, default=None,
                     help="outputs per launch (full domain; bench.py's profiled_traffic key)")
     a = ap.parse_args()
@@ -39,12 +42,17 @@ def main():
         for row in csv.DictReader(open(f)):
             if a.kernel in row["Kernel_Name"].replace("(anonymous namespace)::", ""):
                 durs.append((int(row["Grid_Size_X"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"]),
-                             row["Kernel_Name"]))
-    grid = max(g for g, _, _ in durs) if durs else None
+                             row["Kernel_Name"], int(row["Start_Timestamp"])))
+    grid = max(d[0] for d in durs) if durs else None
     if durs:
-        sel = [d for g, d, _ in durs if a.total or g == grid]
-        res.update(kernel=durs[0][2], calls=len(sel),
-                   avg_ns=(sum(sel) if a.total else sum(sel) / len(sel)), min_ns=min(sel))
+        durs.sort(key=lambda d: d[3])
+        sel = [d for g, d, _, _ in durs if a.total or g == grid]
+        skipped = 0
+        if not a.total and a.skip and len(sel) > a.skip:
+            skipped, sel = a.skip, sel[a.skip:]
+        res.update(kernel=durs[0][2], calls=len(sel), warmup_launches_skipped=skipped,
+                   avg_ns=(sum(sel) if a.total else sum(sel) / len(sel)), min_ns=min(sel),
+                   max_ns=max(sel))
     sums, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):

@@ -1,5 +1,5 @@
 // valu_issue_microbench.hip -- VALU issue cost (cycles per wave-instruction per
-// SIMD) of the instruction forms the bitsliced AES (csrc/kernels/bs_aes.h)
+// SIMD) of the instruction forms the bitsliced AES (tools/bs_aes.h)
 // uses, 4 waves per SIMD, 16 independent accumulators, inline asm so the
 // compiler cannot fold anything.  Clock from the cycle counter is not used:
 // the result is reported at 2.4 GHz and at the s_memtime-measured clock.

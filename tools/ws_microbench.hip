@@ -13,7 +13,7 @@
 
 #include <vector>
 
-#include "../distributed_point_functions_amd/csrc/kernels/bs_aes.h"
+#include "bs_aes.h"
 #include "../distributed_point_functions_amd/csrc/kernels/dpf_device.h"
 
 #ifndef WS_NT
