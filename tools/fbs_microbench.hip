@@ -34,6 +34,16 @@
 #ifndef FBS_WAVES
 #define FBS_WAVES 2
 #endif
+// FBS_FF_GLB = planes of the feed-forward kept in a per-wave global buffer
+// (after the LDS ones); the rest stay in VGPRs.
+#ifndef FBS_FF_GLB
+#define FBS_FF_GLB 0
+#endif
+// FBS_NO_FF=1: drop the MMO feed-forward (x <- AES(sigma(x))): the engine's
+// compute ceiling without the 128 planes of sigma(x) to keep.
+#ifndef FBS_NO_FF
+#define FBS_NO_FF 0
+#endif
 
 namespace {
 
@@ -50,23 +60,42 @@ __host__ __device__ inline uint32_t mix32(uint32_t x) {
 constexpr int kWavesPerBlock = 4;
 
 struct alignas(16) SharedImage {
+#if FBS_MODE != 2
   fbs::MaskTable mt;
+#endif
   uint32_t ff[kWavesPerBlock][FBS_FF_LDS > 0 ? FBS_FF_LDS : 1][64];
 };
 
-// Feed-forward store: planes [0, FBS_FF_LDS) in the wave's LDS rows, the
-// rest in VGPRs.
+// Feed-forward store: planes [0, FBS_FF_LDS) in the wave's LDS rows,
+// [FBS_FF_LDS, FBS_FF_LDS + FBS_FF_GLB) in the wave's global rows, the rest
+// in VGPRs.
+constexpr int kFFReg = 128 - FBS_FF_LDS - FBS_FF_GLB;
+#if FBS_NO_FF
 struct FF {
   uint32_t (*lds)[64];
+  uint32_t* glb;
   int lane;
-  uint32_t reg[128 - FBS_FF_LDS > 0 ? 128 - FBS_FF_LDS : 1];
+  __device__ void put(int, uint32_t) {}
+  __device__ uint32_t get(int) const { return 0; }
+};
+#else
+struct FF {
+  uint32_t (*lds)[64];
+  uint32_t* glb;  // this lane's column of the wave's [plane][64] rows
+  int lane;
+  uint32_t reg[kFFReg > 0 ? kFFReg : 1];
   __device__ void put(int p, uint32_t v) {
-    if (p < FBS_FF_LDS) lds[p][lane] = v; else reg[p - FBS_FF_LDS] = v;
+    if (p < FBS_FF_LDS) lds[p][lane] = v;
+    else if (p < FBS_FF_LDS + FBS_FF_GLB) glb[(p - FBS_FF_LDS) * 64] = v;
+    else reg[p - FBS_FF_LDS - FBS_FF_GLB] = v;
   }
   __device__ uint32_t get(int p) const {
-    return p < FBS_FF_LDS ? lds[p][lane] : reg[p - FBS_FF_LDS];
+    if (p < FBS_FF_LDS) return lds[p][lane];
+    if (p < FBS_FF_LDS + FBS_FF_GLB) return glb[(p - FBS_FF_LDS) * 64];
+    return reg[p - FBS_FF_LDS - FBS_FF_GLB];
   }
 };
+#endif
 
 struct CKeys {
   __device__ uint32_t first(int p) const { return ((CKB::kb.b[0][p / 8] >> (p % 8)) & 1) ? ~0u : 0u; }
@@ -133,22 +162,30 @@ __device__ __forceinline__ void hash32(uint32_t* s, const fbs::MaskTable* mt, FF
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FBS_WAVES, FBS_WAVES)))
-void fbs_kernel(const fbs::MaskTable* gmt, int iters, uint32_t* out, int full) {
+void fbs_kernel(const fbs::MaskTable* gmt, int iters, uint32_t* out, int full, uint32_t* ffbuf) {
   __shared__ SharedImage sh;
+#if FBS_MODE != 2
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(gmt);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&sh.mt);
     for (int i = threadIdx.x; i < (int)(sizeof(fbs::MaskTable) / 4); i += blockDim.x) dst[i] = src[i];
   }
+#endif
   __syncthreads();
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
   FF ff;
   ff.lds = sh.ff[threadIdx.x >> 6];
   ff.lane = threadIdx.x & 63;
+  ff.glb = ffbuf + (size_t)(gid >> 6) * (FBS_FF_GLB > 0 ? FBS_FF_GLB : 1) * 64 + ff.lane;
   uint32_t s[128];
 #pragma unroll
   for (int p = 0; p < 128; ++p) s[p] = mix32(gid * 128u + p);
-  for (int it = 0; it < iters; ++it) hash32(s, &sh.mt, ff);
+  #if FBS_MODE != 2
+  const fbs::MaskTable* mt = &sh.mt;
+#else
+  const fbs::MaskTable* mt = gmt;
+#endif
+  for (int it = 0; it < iters; ++it) hash32(s, mt, ff);
   if (full) {
 #pragma unroll
     for (int p = 0; p < 128; ++p) out[(size_t)p * gridDim.x * blockDim.x + gid] = s[p];
@@ -176,11 +213,13 @@ int main(int argc, char** argv) {
   int cus = 256;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
 
+  uint32_t* ffb;
+  CK(hipMalloc(&ffb, (size_t)cus * 4 * 64 * FBS_WAVES * 2 * (FBS_FF_GLB > 0 ? FBS_FF_GLB : 1) * 4));
   // Correctness: 256 lanes x 32 blocks, two chained hashes, all planes.
   const int vt = 256;
   uint32_t* d;
   CK(hipMalloc(&d, (size_t)vt * 128 * 4));
-  fbs_kernel<<<1, vt>>>(dmt, 2, d, 1);
+  fbs_kernel<<<1, vt>>>(dmt, 2, d, 1, ffb);
   CK(hipGetLastError());
   std::vector<uint32_t> h((size_t)vt * 128);
   CK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
@@ -194,8 +233,9 @@ int main(int argc, char** argv) {
         e[p / 32] |= ((h[(size_t)p * vt + g] >> b) & 1u) << (p % 32);
       }
       dpf_aes::Block4 x{w[0], w[1], w[2], w[3]};
-      x = dpf_aes::mmo_hash(x, lk, dpf_aes::ArrayRK{rk});
-      x = dpf_aes::mmo_hash(x, lk, dpf_aes::ArrayRK{rk});
+      for (int rep = 0; rep < 2; ++rep)
+        x = FBS_NO_FF ? dpf_aes::encrypt(dpf_aes::sigma(x), lk, dpf_aes::ArrayRK{rk})
+                      : dpf_aes::mmo_hash(x, lk, dpf_aes::ArrayRK{rk});
       if (x.w0 != e[0] || x.w1 != e[1] || x.w2 != e[2] || x.w3 != e[3]) ++bad;
     }
   CK(hipFree(d));
@@ -212,7 +252,7 @@ int main(int argc, char** argv) {
   float best = 1e30f;
   for (int rep = 0; rep < 5; ++rep) {
     CK(hipEventRecord(a));
-    fbs_kernel<<<threads / block, block>>>(dmt, iters, d, 0);
+    fbs_kernel<<<threads / block, block>>>(dmt, iters, d, 0, ffb);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -220,8 +260,8 @@ int main(int argc, char** argv) {
     if (rep && ms < best) best = ms;
   }
   const double blocks = (double)threads * 32 * iters;
-  printf("{\"mode\": %d, \"ff_lds\": %d, \"waves_per_simd\": %d, \"iters\": %d, \"ms\": %.3f, "
-         "\"g_aes_per_s\": %.2f}\n",
-         FBS_MODE, FBS_FF_LDS, FBS_WAVES, iters, best, blocks / best / 1e6);
+  printf("{\"mode\": %d, \"ff_lds\": %d, \"ff_glb\": %d, \"sbox_group\": %d, \"waves_per_simd\": %d, "
+         "\"iters\": %d, \"ms\": %.3f, \"g_aes_per_s\": %.2f}\n",
+         FBS_MODE, FBS_FF_LDS, FBS_FF_GLB, FBS_SBOX_GROUP, FBS_WAVES, iters, best, blocks / best / 1e6);
   return 0;
 }
