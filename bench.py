@@ -13,8 +13,8 @@ library validates the context, uploads the correction words (a few KiB), and
 launches the fused gfx950 expand kernel (ExpandSeeds + HashExpandedSeeds +
 value correction) that writes 2^30 * 8 B = 8 GiB of corrected outputs to HBM.
 Keys are generated on the CPU (out of scope for the GPU) before
-the timed region.  The PCIe-inclusive host-output rate is a DESIGN.md note,
-never `value`.
+the timed region.  The PCIe-inclusive host-output rate (`--host-output`,
+below) is reported beside it, never as `value`.
 
 Multi-GPU (distributed_point_functions_amd/sharding.py): weak
 scaling by subtree prefix.  With N = 2^k ranks the domain is 2^(30 + k); rank r
