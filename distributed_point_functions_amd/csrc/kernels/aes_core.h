@@ -205,17 +205,24 @@ DPF_HD void mmo_hash2(Block4& xa, Block4& xb, const LK& lk, const RKA& ra, const
   xb = Block4{eb.w0 ^ sb.w0, eb.w1 ^ sb.w1, eb.w2 ^ sb.w2, eb.w3 ^ sb.w3};
 }
 
-// N independent encryptions interleaved round by round (ILP N): rk[i]
-// provides chain i's round keys.
-template <int N, class LK, class RK>
-DPF_HD void encryptN(Block4* st, const LK& lk, const RK* rk) {
+// NA + NB independent encryptions interleaved round by round (ILP NA + NB):
+// chain i < NA takes its round keys from ra[i], chain NA + j from rb[j] (two
+// key providers, e.g. a uniform value key beside a per-lane key select).
+template <int NA, int NB, class LK, class RKA, class RKB>
+DPF_HD void encryptAB(Block4* st, const LK& lk, const RKA* ra, const RKB* rb) {
+  constexpr int N = NA + NB;
+  // After full unrolling `i` is a constant, so each chain binds one provider.
+  auto key = [&](int i, int j) { return i < NA ? ra[i < NA ? i : 0](j) : rb[i < NA ? 0 : i - NA](j); };
+  auto mix = [&](int i, uint32_t a, uint32_t b, int j) {
+    return i < NA ? ra[i < NA ? i : 0].mix(lk, a, b, j) : rb[i < NA ? 0 : i - NA].mix(lk, a, b, j);
+  };
   uint32_t w[N][4];
 DPF_UNROLL
   for (int i = 0; i < N; ++i) {
-    w[i][0] = st[i].w0 ^ rk[i](0);
-    w[i][1] = st[i].w1 ^ rk[i](1);
-    w[i][2] = st[i].w2 ^ rk[i](2);
-    w[i][3] = st[i].w3 ^ rk[i](3);
+    w[i][0] = st[i].w0 ^ key(i, 0);
+    w[i][1] = st[i].w1 ^ key(i, 1);
+    w[i][2] = st[i].w2 ^ key(i, 2);
+    w[i][3] = st[i].w3 ^ key(i, 3);
   }
 #if defined(__HIP_DEVICE_COMPILE__)
   DPF_ROUND_LOOP
@@ -233,7 +240,7 @@ DPF_UNROLL
     for (int i = 0; i < N; ++i) {
 DPF_UNROLL
       for (int c = 0; c < 4; ++c)
-        n[i][c] = rk[i].mix(lk, n[i][c], lk.template lookup<3, 3>(w[i][(c + 3) & 3]), 4 * r + c);
+        n[i][c] = mix(i, n[i][c], lk.template lookup<3, 3>(w[i][(c + 3) & 3]), 4 * r + c);
     }
 DPF_UNROLL
     for (int i = 0; i < N; ++i)
@@ -249,10 +256,10 @@ DPF_UNROLL
   };
 DPF_UNROLL
   for (int i = 0; i < N; ++i) {
-    st[i] = Block4{last(w[i][0], w[i][1], w[i][2], w[i][3], rk[i](40)),
-                   last(w[i][1], w[i][2], w[i][3], w[i][0], rk[i](41)),
-                   last(w[i][2], w[i][3], w[i][0], w[i][1], rk[i](42)),
-                   last(w[i][3], w[i][0], w[i][1], w[i][2], rk[i](43))};
+    st[i] = Block4{last(w[i][0], w[i][1], w[i][2], w[i][3], key(i, 40)),
+                   last(w[i][1], w[i][2], w[i][3], w[i][0], key(i, 41)),
+                   last(w[i][2], w[i][3], w[i][0], w[i][1], key(i, 42)),
+                   last(w[i][3], w[i][0], w[i][1], w[i][2], key(i, 43))};
 #if defined(__HIP_DEVICE_COMPILE__)
     // Keeps the scheduler from issuing all N chains' last-round lookups before
     // any is consumed: at ILP4 the 64 live results spilled at 128 VGPRs (the
@@ -263,6 +270,13 @@ DPF_UNROLL
   }
 }
 
+// N independent encryptions interleaved round by round (ILP N): rk[i]
+// provides chain i's round keys.
+template <int N, class LK, class RK>
+DPF_HD void encryptN(Block4* st, const LK& lk, const RK* rk) {
+  encryptAB<N, 0>(st, lk, rk, rk);
+}
+
 // N MMO hashes interleaved.
 template <int N, class LK, class RK>
 DPF_HD void mmo_hashN(Block4* x, const LK& lk, const RK* rk) {
@@ -270,6 +284,19 @@ DPF_HD void mmo_hashN(Block4* x, const LK& lk, const RK* rk) {
 DPF_UNROLL
   for (int i = 0; i < N; ++i) e[i] = s[i] = sigma(x[i]);
   encryptN<N>(e, lk, rk);
+DPF_UNROLL
+  for (int i = 0; i < N; ++i)
+    x[i] = Block4{e[i].w0 ^ s[i].w0, e[i].w1 ^ s[i].w1, e[i].w2 ^ s[i].w2, e[i].w3 ^ s[i].w3};
+}
+
+// NA + NB MMO hashes interleaved (encryptAB's key providers).
+template <int NA, int NB, class LK, class RKA, class RKB>
+DPF_HD void mmo_hashAB(Block4* x, const LK& lk, const RKA* ra, const RKB* rb) {
+  constexpr int N = NA + NB;
+  Block4 s[N], e[N];
+DPF_UNROLL
+  for (int i = 0; i < N; ++i) e[i] = s[i] = sigma(x[i]);
+  encryptAB<NA, NB>(e, lk, ra, rb);
 DPF_UNROLL
   for (int i = 0; i < N; ++i)
     x[i] = Block4{e[i].w0 ^ s[i].w0, e[i].w1 ^ s[i].w1, e[i].w2 ^ s[i].w2, e[i].w3 ^ s[i].w3};

@@ -29,7 +29,9 @@
 // registers, then adds them once into exact 192-bit per-element sums.
 // No last-round scheduling fence in this TU (aes_core.h, encryptN): the
 // heavy-hitters kernel measured 0.35% slower with it (24.26 vs 24.18 s per pass).
+#ifndef DPF_LAST_ROUND_FENCE
 #define DPF_LAST_ROUND_FENCE 1024
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -734,221 +736,3 @@ int dpf_hip_gather_batched(int64_t num_keys, int64_t in_row_elems, int64_t num_r
 }
 
 }  // extern "C"
-
-// ==========================================================================
-// Batched DCF evaluation
-// ==========================================================================
-// DistributedComparisonFunction::Evaluate (dcf/distributed_comparison_function
-// .h:83-105) sums, over the hierarchy levels i < n with bit (n-1-i) of x
-// clear, EvaluateAt(key, i, {x >> (n - i)}) of an n-level incremental DPF
-// whose level i has log domain i.  Level i's point lies on x's path at tree
-// depth D_i, and D_i grows by at most one per level, so ONE walk down x's
-// path visits every level: at depth d the node's value hash serves each level
-// with D_i == d (element (x >> (n-i)) mod 2^(i - d) of the converted block),
-// and the next path step hashes the same node -- the two are interleaved.
-// The reference walks from the root once per level (n^2/2 AES); this is n + n.
-// For n == 128 the reference evaluates every level at prefix 0 (its
-// `if (log_domain_size < 128)` guard); that is mirrored.
-namespace {
-
-constexpr int kDcfMaxLevels = 128;
-constexpr int kDcfMaxLeaves = 4;
-
-struct DcfLevels {
-  int n;                              // hierarchy levels = DCF log domain size
-  uint8_t depth[kDcfMaxLevels];       // hierarchy_to_tree
-  uint8_t blocks[kDcfMaxLevels];      // blocks_needed per level
-  const dpf_block* vcw[kDcfMaxLevels];  // per level: [key][E * num_leaves]
-};
-
-struct DcfParams {
-  int64_t num_keys, points_per_key, num_items;
-  int shared_points;
-  int cw_stride;
-  int vcw_stride;  // E * num_leaves
-  int esz;
-  int xor_mode;
-  const dpf_block* key_seed;
-  const uint8_t* party;
-  const dpf_block* points;
-  const dpf_block* cw_seed;
-  const uint8_t* cw_left;
-  const uint8_t* cw_right;
-  char* out;
-  RoundKeys rkl, rkd, rkv;
-};
-
-__device__ __forceinline__ u128 shr128(u128 x, int s) { return s >= 128 ? (u128)0 : x >> s; }
-
-template <int BITS, bool FAST>
-__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
-    DcfParams p, DcfLevels lv, GenericLeaf g) {
-  __shared__ LdsImage lds;
-  fill_tables(lds.tab);
-  __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
-  const int n = lv.n;
-  const int dmax = lv.depth[n - 1];
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
-       u += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = u / p.points_per_key, j = u - k * p.points_per_key;
-    const u128 x = dpf_u128(p.points[p.shared_points ? j : u]);
-    const int party = p.party[k] & 1;
-    Block4 s = load_block(p.key_seed + k);
-    uint32_t t = (uint32_t)party;
-    const dpf_block* cws = p.cw_seed + k * p.cw_stride;
-    const uint8_t* cl = p.cw_left + k * p.cw_stride;
-    const uint8_t* cr = p.cw_right + k * p.cw_stride;
-    u128 acc[FAST ? 1 : kDcfMaxLeaves];
-    const int nl = FAST ? 1 : g.d.num_leaves;
-    for (int e = 0; e < nl; ++e) acc[e] = 0;
-    int level = 0;
-    for (int d = 0; d <= dmax; ++d) {
-      // Next node on x's path (computed beside the value hash when FAST).
-      const uint32_t bit = d < dmax && n < 128 ? (uint32_t)(shr128(x, n - d - 1) & 1) : 0u;
-      Block4 hv = s, hn = s;
-      if (FAST) {
-        if (d < dmax)
-          dpf_aes::mmo_hash2(hv, hn, lk, UniformRK{p.rkv.k}, SelectRK{p.rkl.k, p.rkd.k, 0u - bit});
-        else
-          hv = dpf_aes::mmo_hash(s, lk, UniformRK{p.rkv.k});
-      }
-      for (; level < n && lv.depth[level] == d; ++level) {
-        const bool take = ((shr128(x, n - 1 - level)) & 1) == 0;  // current_bit == 0
-        const u128 prefix = n < 128 ? shr128(x, n - level) : (u128)0;
-        const int bi = (int)(prefix & (((u128)1 << (level - d)) - 1));
-        const dpf_block* vcw = lv.vcw[level] + k * p.vcw_stride;
-        if (FAST) {
-          const u128 v = fast_point_value<BITS>(hv, t, bi, dpf_u128(vcw[bi]), party, p.xor_mode);
-          if (take) {
-            if (p.xor_mode) acc[0] ^= v; else acc[0] += v;
-          }
-        } else {
-          GenericLeaf lf = g;
-          lf.d.blocks_needed = lv.blocks[level];
-          lf.vcw = vcw;
-          lf.party = party;
-          char buf[16 * kDcfMaxLeaves];
-          lf.convert_store(lk, p.rkv.k, s, t, bi, 1, buf);
-          int off = 0;
-          for (int e = 0; e < nl; ++e) {
-            const int lb = g.d.bits[e] >> 3;
-            const u128 v = GenericLeaf::load_le(reinterpret_cast<const uint8_t*>(buf) + off, lb);
-            off += lb;
-            if (take) acc[e] = leaf_group_add(g.d, e, acc[e], v);
-          }
-        }
-      }
-      if (d == dmax) break;
-      const dpf_block c = cws[d];
-      const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
-                                  (uint32_t)(c.high >> 32));
-      const uint32_t cctl = (uint32_t)(cl[d] & 1) | ((uint32_t)(cr[d] & 1) << 1);
-      if (FAST) {
-        const uint32_t m = 0u - t;
-        hn.w0 ^= cs.x & m; hn.w1 ^= cs.y & m; hn.w2 ^= cs.z & m; hn.w3 ^= cs.w & m;
-        const uint32_t nt = (hn.w0 & 1u) ^ (t & ((cctl >> bit) & 1u));
-        hn.w0 &= ~1u;
-        s = hn;
-        t = nt;
-      } else {
-        path_step(lk, p.rkl, p.rkd, s, t, bit, cs, cctl);
-      }
-    }
-    char* o = p.out + u * (int64_t)p.esz;
-    if (FAST) {
-      store_bits<BITS>(o, acc[0]);
-    } else {
-      for (int e = 0; e < nl; ++e) {
-        const int lb = g.d.bits[e] >> 3;
-        GenericLeaf::store_le(o, acc[e], lb);
-        o += lb;
-      }
-    }
-  }
-}
-
-}  // namespace
-
-extern "C" int dpf_hip_dcf_eval_batch(int64_t num_keys, int64_t points_per_key, int shared_points,
-                                      int num_levels, const int32_t* level_depth,
-                                      const int32_t* level_blocks, const dpf_block* key_seed,
-                                      const uint8_t* party, const dpf_block* points,
-                                      const dpf_block* cw_seed, const uint8_t* cw_left,
-                                      const uint8_t* cw_right, int cw_stride,
-                                      const dpf_block* const* value_correction,
-                                      const dpf_aes_key* key_left, const dpf_aes_key* key_right,
-                                      const dpf_aes_key* key_value, const dpf_value_desc* desc,
-                                      void* out, void* stream) {
-  int st = validate_desc(desc);
-  if (st) return st;
-  if (num_keys < 0 || points_per_key < 0 || num_levels < 1 || num_levels > kDcfMaxLevels)
-    return fail(kInvalidArgument, "num_keys, points_per_key or num_levels out of range");
-  if (!level_depth || !level_blocks || !value_correction)
-    return fail(kInvalidArgument, "NULL level table");
-  DcfLevels lv;
-  memset(&lv, 0, sizeof(lv));
-  lv.n = num_levels;
-  for (int i = 0; i < num_levels; ++i) {
-    const int dep = level_depth[i];
-    if (dep < 0 || dep > i || (i > 0 && (dep < level_depth[i - 1] || dep > level_depth[i - 1] + 1)) ||
-        (i == 0 && dep != 0) || dep >= cw_stride + 1 || i - dep > 7)
-      return fail(kInvalidArgument, "level depths are not a DCF hierarchy");
-    if (level_blocks[i] < 1 || level_blocks[i] > kBMax)
-      return fail(kUnimplemented, "value type needs too many AES blocks for the GPU path");
-    if (!value_correction[i]) return fail(kInvalidArgument, "NULL value correction");
-    lv.depth[i] = (uint8_t)dep;
-    lv.blocks[i] = (uint8_t)level_blocks[i];
-    lv.vcw[i] = value_correction[i];
-  }
-  if (lv.depth[num_levels - 1] > cw_stride) return fail(kInvalidArgument, "cw_stride too small");
-  const bool fast = fast_int(desc);
-  if (!fast && desc->num_leaves > kDcfMaxLeaves)
-    return fail(kUnimplemented, "DCF value type has too many leaves for the GPU path");
-  const int64_t items = num_keys * points_per_key;
-  if (items == 0) return kOk;
-  if (!key_seed || !party || !points || !out || !key_left || !key_right || !key_value ||
-      (lv.depth[num_levels - 1] > 0 && (!cw_seed || !cw_left || !cw_right)))
-    return fail(kInvalidArgument, "NULL pointer");
-  DcfParams p;
-  memset(&p, 0, sizeof(p));
-  p.num_keys = num_keys;
-  p.points_per_key = points_per_key;
-  p.num_items = items;
-  p.shared_points = shared_points ? 1 : 0;
-  p.cw_stride = cw_stride;
-  p.vcw_stride = desc->elements_per_block * desc->num_leaves;
-  p.esz = packed_size(desc);
-  p.xor_mode = desc->kind[0] == DPF_LEAF_XOR;
-  p.key_seed = key_seed;
-  p.party = party;
-  p.points = points;
-  p.cw_seed = cw_seed;
-  p.cw_left = cw_left;
-  p.cw_right = cw_right;
-  p.out = (char*)out;
-  p.rkl = expand_key(key_left);
-  p.rkd = xor_keys(p.rkl, expand_key(key_right));
-  p.rkv = expand_key(key_value);
-  GenericLeaf g;
-  memset(&g, 0, sizeof(g));
-  g.d = *desc;
-  g.elements_per_leaf = 1;
-  g.esz = p.esz;
-  hipStream_t s = (hipStream_t)stream;
-  const int blk = block_for(items);
-  const dim3 grid(grid_for(items, blk)), block(blk);
-  if (fast) {
-    switch (desc->bits[0]) {
-      case 8: hipLaunchKernelGGL((dcf_eval_kernel<8, true>), grid, block, 0, s, p, lv, g); break;
-      case 16: hipLaunchKernelGGL((dcf_eval_kernel<16, true>), grid, block, 0, s, p, lv, g); break;
-      case 32: hipLaunchKernelGGL((dcf_eval_kernel<32, true>), grid, block, 0, s, p, lv, g); break;
-      case 64: hipLaunchKernelGGL((dcf_eval_kernel<64, true>), grid, block, 0, s, p, lv, g); break;
-      default: hipLaunchKernelGGL((dcf_eval_kernel<128, true>), grid, block, 0, s, p, lv, g); break;
-    }
-  } else {
-    hipLaunchKernelGGL((dcf_eval_kernel<8, false>), grid, block, 0, s, p, lv, g);
-  }
-  HIP_TRY(hipGetLastError());
-  return kOk;
-}

@@ -108,3 +108,75 @@ def test_dcf_errors_match_reference():
         dcf.evaluate_packed(k0, [64])
     with pytest.raises(D.DpfStatusError, match="Value type T doesn't match"):
         dcf.evaluate(k0, 3, D.integer_type(64))
+
+
+def _batch_case(vt, n, nk, ppk, shared, seed):
+    import torch
+    dcf = make(vt, n)
+    P = O.dcf_params(n, vt)
+    rng = np.random.default_rng(seed)
+    beta = [int(b) for b in rng.integers(1, 100, size=len(O.leaves(vt)))]
+    alphas = [int(a) for a in rng.integers(0, 1 << min(n, 63), size=nk)]
+    keys = [dcf.generate_keys(a, leaves_value(vt, beta), seed_0=2 * k + 1, seed_1=2 * k + 2)[k % 2]
+            for k, a in enumerate(alphas)]
+    npts = ppk if shared else nk * ppk
+    hi = 1 << min(n, 127)
+    pts = [int(x) for x in rng.integers(0, min(hi, 2**63), size=npts)]
+    # Points near each key's alpha as well, so both comparison outcomes occur.
+    if not shared:
+        for k in range(nk):
+            pts[k * ppk] = alphas[k]
+            pts[k * ppk + 1] = max(alphas[k] - 1, 0)
+    dev = dcf.upload_key_batch(dcf.make_key_batch(keys))
+    dpts = torch.from_numpy(D.u128_array(pts).view(np.int64)).cuda()
+    size = dcf.packed_size()
+
+    def run():
+        out = torch.empty(nk * ppk * size, dtype=torch.uint8, device="cuda")
+        assert dcf.evaluate_batch_to_device(dev, dpts, ppk, out, shared_points=shared) == nk * ppk
+        return out.cpu().numpy().reshape(nk, ppk, size)
+
+    return dcf, P, beta, alphas, pts, run
+
+
+FAST_TYPES = [("int", 8), ("int", 16), ("int", 32), ("int", 64), ("int", 128), ("xor", 32),
+              ("xor", 64)]
+
+
+@pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
+@pytest.mark.parametrize("n,shared", [(17, False), (64, True), (128, False)], ids=str)
+def test_dcf_fast_kernel_uniform_keys(vt, n, shared, monkeypatch):
+    """dcf_fast_kernel with wave-uniform keys (points_per_key % 64 == 0) is
+    bit-exact against the general kernel on every output and against the
+    oracle on sampled rows."""
+    nk, ppk = 24, 128
+    dcf, P, beta, alphas, pts, run = _batch_case(vt, n, nk, ppk, shared, seed=n * 7 + len(vt))
+    got = run()
+    monkeypatch.setenv("DPF_DCF_GENERAL", "1")
+    general = run()
+    np.testing.assert_array_equal(got, general)
+    rng = np.random.default_rng(3)
+    for k in (0, nk - 1):
+        okeys = O.dcf_generate_keys(P, alphas[k], beta, 2 * k + 1, 2 * k + 2)
+        for j in [0, 1] + [int(q) for q in rng.integers(0, ppk, size=6)]:
+            x = pts[j] if shared else pts[k * ppk + j]
+            np.testing.assert_array_equal(got[k, j], O.dcf_evaluate(P, okeys[k % 2], x).reshape(-1),
+                                          err_msg=f"key {k} point {j}")
+
+
+@pytest.mark.parametrize("vt", [("int", 64), ("xor", 32), ("int", 8)], ids=str)
+def test_dcf_fast_kernel_full_launch(vt, monkeypatch):
+    """A launch that fills the chip twice over (512 keys x 1024 points):
+    bit-exact against the general kernel on every output and against the
+    oracle on sampled rows."""
+    nk, ppk, n = 512, 1024, 64
+    dcf, P, beta, alphas, pts, run = _batch_case(vt, n, nk, ppk, False, seed=99)
+    got = run()
+    monkeypatch.setenv("DPF_DCF_GENERAL", "1")
+    general = run()
+    np.testing.assert_array_equal(got, general)
+    for k in (0, 1, nk - 1):
+        okeys = O.dcf_generate_keys(P, alphas[k], beta, 2 * k + 1, 2 * k + 2)
+        for j in (0, 1, 2, 700, ppk - 1):
+            np.testing.assert_array_equal(got[k, j],
+                                          O.dcf_evaluate(P, okeys[k % 2], pts[k * ppk + j]).reshape(-1))

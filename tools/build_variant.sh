@@ -11,7 +11,8 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -mcode-object-version=5 -Iinclude"
 for src in $K/*.hip; do
   b=$(basename $src .hip)
   sched="-mllvm -amdgpu-sched-strategy=${DPF_SCHED:-iterative-ilp}"
-  { [ "$b" = dpf_batch ] || [ "$b" = dpf_expand_hybrid ] || [ "$b" = dpf_expand_ws ]; } && sched=""
+  # dpf_batch.hip uses the default scheduler unless DPF_BATCH_ILP=1.
+  [ "$b" = dpf_batch ] && [ "${DPF_BATCH_ILP:-0}" != 1 ] && sched=""
   /opt/rocm/bin/hipcc $F $sched "$@" -c $src -o $out/$b.o &
 done
 wait
