@@ -216,6 +216,13 @@ struct Mod32V {
     for (int i = 0; i < NLMAX; ++i) c[i] = i < nl ? (uint32_t)v[i].low : 0u;
   }
   __device__ __forceinline__ void convert(const uint32_t* w, uint32_t t, Val& out) const {
+#if defined(DPF_PROBE_NO_CONVERT)
+    // Probe build only (tools/): the sampling's divisions left out, so a run
+    // measures what the rest of the kernel costs.  Outputs are NOT the DPF's.
+#pragma unroll
+    for (int i = 0; i < NLMAX; ++i) out.x[i] = (w[i] + (t ? c[i] : 0u)) ^ (uint32_t)party;
+    return;
+#endif
     uint32_t blk[4] = {w[0], w[1], w[2], w[3]};
 #pragma unroll
     for (int i = 0; i < NLMAX; ++i) {
