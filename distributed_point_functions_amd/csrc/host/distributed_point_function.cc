@@ -21,6 +21,8 @@
 namespace distributed_point_functions {
 
 using dpf_internal::AesKey;
+using dpf_internal::CopyToHostSink;
+using dpf_internal::CopyToHostVector;
 using dpf_internal::PackedUploads;
 using dpf_internal::FromBlock;
 using dpf_internal::FromHip;
@@ -614,8 +616,8 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   }
   if (!device_out) {
     const size_t bytes = static_cast<size_t>(total) * esz;
-    void* dst = (*host_out)(bytes);
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(dst, result, bytes, stream));
+    void* dst = host_out->reserve(bytes);
+    HIP_RETURN_IF_ERROR(CopyToHostSink(*host_out, dst, result, bytes, stream));
   }
   return OkStatus();
 }
@@ -625,10 +627,7 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateUntilPacked(
     const ValueType* requested_type) const {
   std::vector<uint8_t> out;
   int64_t n = 0;
-  const HostSink sink = [&out](size_t bytes) -> void* {
-    out = dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(bytes));
-    return out.data();
-  };
+  const HostSink sink = dpf_internal::VectorSink(&out);
   DPF_RETURN_IF_ERROR(EvaluateUntilCore(hierarchy_level, prefixes, ctx, requested_type, nullptr, 0,
                                         nullptr, &sink, &n));
   return out;
@@ -788,9 +787,9 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
       up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), s->out.get(),
       nullptr));
   DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
-  std::vector<uint8_t> out =
-      dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(n) * f.packed_size);
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
+  std::vector<uint8_t> out;
+  HIP_RETURN_IF_ERROR(CopyToHostVector(&out, s->out.get(),
+                                       static_cast<size_t>(n) * f.packed_size, nullptr));
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return out;
 }
@@ -858,9 +857,9 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtBatchPacked(
       s->paths.as<dpf_block>(), s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(),
       s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc,
       s->vcw.as<dpf_block>(), s->out.get(), nullptr));
-  std::vector<uint8_t> out =
-      dpf_internal::MakeOutputVector<uint8_t>(static_cast<int64_t>(n) * f.packed_size);
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
+  std::vector<uint8_t> out;
+  HIP_RETURN_IF_ERROR(CopyToHostVector(&out, s->out.get(),
+                                       static_cast<size_t>(n) * f.packed_size, nullptr));
   return out;
 }
 

@@ -34,6 +34,25 @@ inline Status FromHip(int code) {
 }
 #define HIP_RETURN_IF_ERROR(expr) DPF_RETURN_IF_ERROR(::distributed_point_functions::dpf_internal::FromHip(expr))
 
+// Copies `bytes` of device output into the storage `dst` a HostSink reserved,
+// letting its grow() initialise each chunk right before that chunk's DMA
+// (dpf_hip_memcpy_d2h_staged).  Returns a dpf_hip status code.
+inline int CopyToHostSink(const HostSink& sink, void* dst, const void* src, size_t bytes,
+                          void* stream) {
+  if (!sink.grow) return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
+  auto before = [](void* ctx, size_t ready) {
+    (*static_cast<const std::function<void(size_t)>*>(ctx))(ready);
+  };
+  return dpf_hip_memcpy_d2h_staged(dst, src, bytes, before,
+                                   const_cast<std::function<void(size_t)>*>(&sink.grow), stream);
+}
+
+// `bytes` of device memory into a fresh host vector.
+inline int CopyToHostVector(std::vector<uint8_t>* out, const void* src, size_t bytes, void* stream) {
+  const HostSink sink = VectorSink(out);
+  return CopyToHostSink(sink, sink.reserve(bytes), src, bytes, stream);
+}
+
 inline dpf_block ToBlock(uint128 v) { return dpf_block{Uint128Low64(v), Uint128High64(v)}; }
 inline uint128 FromBlock(const dpf_block& b) { return MakeUint128(b.high, b.low); }
 inline uint128 FromProtoBlock(const Block& b) { return MakeUint128(b.high(), b.low()); }

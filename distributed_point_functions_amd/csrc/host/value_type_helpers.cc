@@ -384,6 +384,16 @@ void AdviseHugePages(void* p, size_t bytes) {
   if (hi > lo) (void)madvise(reinterpret_cast<void*>(lo), hi - lo, MADV_HUGEPAGE);
 }
 
+void PrefaultPages(void* p, size_t bytes) {
+  if (!p || bytes < (size_t{64} << 20)) return;
+  constexpr size_t kPage = 4096;
+  volatile char* base = static_cast<char*>(p);
+  const int64_t pages = static_cast<int64_t>(bytes / kPage);
+  ParallelChunks(pages, NumChunks(pages, 4096), [base](int, int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) base[i * kPage] = 0;
+  });
+}
+
 void ParallelRanges(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
   ParallelChunks(n, NumChunks(n, grain), [&fn](int, int64_t lo, int64_t hi) { fn(lo, hi); });
 }

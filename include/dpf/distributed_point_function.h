@@ -154,10 +154,7 @@ class DistributedPointFunction {
       // The packed elements are T's memory image: copy them from the device
       // straight into the result.
       std::vector<T> out;
-      const HostSink sink = [&out](size_t bytes) -> void* {
-        out = dpf_internal::MakeOutputVector<T>(static_cast<int64_t>(bytes / sizeof(T)));
-        return out.data();
-      };
+      const HostSink sink = dpf_internal::VectorSink(&out);
       Status status = EvaluateUntilToHost(hierarchy_level, prefixes, ctx, &t, sink);
       if (!status.ok()) return status;
       return out;
@@ -200,9 +197,9 @@ class DistributedPointFunction {
 
   // ---- type-erased core (packed elements) --------------------------------
   // `requested_type` (may be null) plays the role of T in the templates.
-  // A HostSink is called once with the output size in bytes and returns where
-  // the packed output is to be copied.
-  using HostSink = std::function<void*(size_t bytes)>;
+  // Where the packed output is copied (dpf_internal::HostSink: storage for it,
+  // and how a fresh vector becomes valid chunk by chunk during the copy).
+  using HostSink = dpf_internal::HostSink;
   Status EvaluateUntilToHost(int hierarchy_level, Span<const uint128> prefixes,
                              EvaluationContext& ctx, const ValueType* requested_type,
                              const HostSink& sink) const;

@@ -257,15 +257,51 @@ constexpr bool kPackedIsMemoryImage =
 // faults on the GPU box's host, ~7 ms with 2 MiB pages.  No-op below 4 MiB.
 void AdviseHugePages(void* p, size_t bytes);
 
+// Maps the pages of fresh storage [p, p + bytes) by touching them on up to 16
+// host threads.  8 GiB: 30-47 ms, where the page faults of a one-thread
+// first touch (value-initialisation) cost ~350 of the ~500 ms it takes
+// (tools/host_output_microbench.cc).  No-op below 64 MiB.
+void PrefaultPages(void* p, size_t bytes);
+
+// Storage of a fresh std::vector<T> of n elements, reserved, advised onto huge
+// pages and pre-faulted, but still empty (size 0).
+template <typename T>
+void ReserveOutputVector(std::vector<T>& out, int64_t n) {
+  out.clear();
+  out.reserve(n);
+  AdviseHugePages(out.data(), static_cast<size_t>(n) * sizeof(T));
+  PrefaultPages(out.data(), static_cast<size_t>(n) * sizeof(T));
+}
+
 // A value-initialised std::vector<T> of n elements whose storage was advised
-// onto huge pages before the initialisation touched it.
+// onto huge pages and mapped on the host threads before the (one-thread)
+// initialisation touched it.
 template <typename T>
 std::vector<T> MakeOutputVector(int64_t n) {
   std::vector<T> out;
-  out.reserve(n);
-  AdviseHugePages(out.data(), static_cast<size_t>(n) * sizeof(T));
+  ReserveOutputVector(out, n);
   out.resize(n);
   return out;
+}
+
+// Where a packed device output is copied on the host (EvaluateUntilToHost):
+// reserve(bytes) returns storage for it; grow(bytes) (may be empty) makes its
+// first `bytes` bytes valid and is called chunk by chunk right before each
+// chunk's DMA, so a fresh vector's value-initialisation overlaps the copy
+// (dpf_hip_memcpy_d2h_staged).
+struct HostSink {
+  std::function<void*(size_t bytes)> reserve;
+  std::function<void(size_t bytes)> grow;
+};
+
+// The HostSink that fills a fresh std::vector<T> (bytes: a multiple of sizeof(T)).
+template <typename T>
+HostSink VectorSink(std::vector<T>* out) {
+  return HostSink{[out](size_t bytes) -> void* {
+                    ReserveOutputVector(*out, static_cast<int64_t>(bytes / sizeof(T)));
+                    return out->data();
+                  },
+                  [out](size_t bytes) { out->resize((bytes + sizeof(T) - 1) / sizeof(T)); }};
 }
 
 // fn(lo, hi) over [0, n) in chunks of at least `grain`, on up to 16 host threads.

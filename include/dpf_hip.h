@@ -90,6 +90,16 @@ int dpf_hip_host_alloc(void** ptr, size_t bytes);
 int dpf_hip_host_free(void* ptr);
 int dpf_hip_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+/* D2H copy into FRESH host storage that the caller initialises chunk by chunk
+ * (e.g. a std::vector<T> being value-initialised by resize): before each
+ * chunk's DMA, `before_chunk(ctx, bytes_ready)` is called and must make
+ * [0, bytes_ready) of `dst` valid; the DMA of one chunk overlaps the
+ * initialisation of the next.  Large copies DMA straight into `dst`
+ * (registered for the copy), others go through page-locked staging.  The
+ * drop-in EvaluateUntil<T> returns its std::vector<T> this way. */
+int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
+                              void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
+                              void* stream);
 int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memset(void* dst, int value, size_t bytes, void* stream);
 int dpf_hip_stream_sync(void* stream);

@@ -360,3 +360,27 @@ def test_evaluate_shard_to_device_errors():
     dpf2.evaluate_until(0, [], ctx)
     with pytest.raises(D.DpfStatusError, match="first call"):
         dpf2.evaluate_shard_to_device(1, 0, 2, ctx, dev)
+
+
+@pytest.mark.parametrize("log,vt", [(26, ("int", 64)), (25, ("int", 128)),
+                                    (24, ("tuple", [("int", 32), ("int", 64)]))], ids=str)
+def test_large_host_output_matches_device(log, vt):
+    """Host outputs of >= 32 MiB take dpf_hip_memcpy_d2h_staged: the fresh
+    vector is registered and value-initialised chunk by chunk while the
+    previous 64 MiB chunk's DMA runs.  Every byte equals the device output,
+    and the two parties' host outputs reconstruct the point function."""
+    import torch
+    dpf = E.params([(log, vt, 0)])
+    alpha = (1 << log) - 12345
+    beta = [[7]] if vt[0] == "int" else [[3, 9]]
+    k0, k1 = E.generate_keys(dpf, alpha, beta, (11, 12))
+    host0 = dpf.evaluate_until(0, [], dpf.create_evaluation_context(k0), packed=True)
+    host1 = dpf.evaluate_until(0, [], dpf.create_evaluation_context(k1), packed=True)
+    dev = torch.empty(host0.size, dtype=torch.uint8, device="cuda")
+    n = dpf.evaluate_until_to_device(0, [], dpf.create_evaluation_context(k0), dev)
+    torch.cuda.synchronize()
+    assert n == 1 << log
+    np.testing.assert_array_equal(dev.cpu().numpy().reshape(host0.shape), host0)
+    total = O.add_packed(vt, host0.reshape(1 << log, -1), host1.reshape(1 << log, -1))
+    nz = np.flatnonzero(total.reshape(1 << log, -1).any(axis=1))
+    assert nz.tolist() == [alpha]
