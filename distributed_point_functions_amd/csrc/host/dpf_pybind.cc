@@ -65,11 +65,15 @@ uint128 IntToU128(const py::int_& x) {
   return MakeUint128(hi, lo);
 }
 
-py::array_t<uint8_t> ToArray(const std::vector<uint8_t>& v) {
-  py::array_t<uint8_t> a(static_cast<py::ssize_t>(v.size()));
-  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size());
-  return a;
+// The result vector itself becomes the numpy array's storage (no copy: a
+// multi-GiB output would otherwise be faulted in and copied on one thread).
+py::array_t<uint8_t> ToArray(std::vector<uint8_t>&& v) {
+  auto* owned = new std::vector<uint8_t>(std::move(v));
+  py::capsule free_when_done(owned, [](void* p) { delete static_cast<std::vector<uint8_t>*>(p); });
+  return py::array_t<uint8_t>({static_cast<py::ssize_t>(owned->size())}, {py::ssize_t{1}},
+                              owned->data(), free_when_done);
 }
+py::array_t<uint8_t> ToArray(const std::vector<uint8_t>& v) { return ToArray(std::vector<uint8_t>(v)); }
 
 std::unique_ptr<ValueType> OptType(const py::object& o) {
   if (o.is_none()) return nullptr;
@@ -188,7 +192,7 @@ class PyDpf {
       }
       out = std::move(*r);
     }
-    return py::make_tuple(ToArray(out), Ser(ctx));
+    return py::make_tuple(ToArray(std::move(out)), Ser(ctx));
   }
   py::tuple EvaluateUntilToDevice(int level,
                                   const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& prefixes,
@@ -243,7 +247,7 @@ class PyDpf {
     auto p = ToU128(points);
     auto t = OptType(vt);
     auto out = Take(dpf_->EvaluateAtPacked(ctx.key(), level, MakeConstSpan(p), &ctx, t.get()));
-    return py::make_tuple(ToArray(out), Ser(ctx));
+    return py::make_tuple(ToArray(std::move(out)), Ser(ctx));
   }
   py::array_t<uint8_t> EvaluateAtBatch(const std::vector<py::bytes>& keys, int level,
                                        const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& points,

@@ -384,3 +384,18 @@ def test_large_host_output_matches_device(log, vt):
     total = O.add_packed(vt, host0.reshape(1 << log, -1), host1.reshape(1 << log, -1))
     nz = np.flatnonzero(total.reshape(1 << log, -1).any(axis=1))
     assert nz.tolist() == [alpha]
+
+
+def test_concurrent_large_host_outputs():
+    """Four threads evaluate different keys into fresh host vectors at once
+    (the registered-DMA path of >= 32 MiB outputs runs concurrently, GIL
+    released): every result equals the same key's sequential result."""
+    from concurrent.futures import ThreadPoolExecutor
+    dpf = E.params([(24, ("int", 64), 0)])
+    keys = [E.generate_keys(dpf, 1000 + 7 * i, [[i + 1]], (20 + i, 40 + i))[i % 2] for i in range(4)]
+    want = [dpf.evaluate_until(0, [], dpf.create_evaluation_context(k), packed=True) for k in keys]
+    with ThreadPoolExecutor(4) as ex:
+        got = list(ex.map(lambda k: dpf.evaluate_until(0, [], dpf.create_evaluation_context(k),
+                                                         packed=True), keys * 2))
+    for i, g in enumerate(got):
+        np.testing.assert_array_equal(g, want[i % 4])
