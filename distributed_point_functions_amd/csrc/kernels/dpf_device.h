@@ -430,6 +430,17 @@ __device__ __forceinline__ uint32_t div_2by1(uint32_t u1, uint32_t u0, uint32_t 
 // 128-bit block w (little-endian words) -> remainder mod N, and the low three
 // quotient words (what `quotient << 32` keeps of it, int_mod_n.h:167-176).
 __device__ __forceinline__ uint32_t divmod128(const uint32_t w[4], const Div32& d, uint32_t q[3]) {
+  if (d.sh == 0) {
+    // N >= 2^31 (e.g. 2^32 - 5): no normalisation shifts, and the top word's
+    // quotient digit (0 or 1, shifted out) is one compare.  `d` is a kernel
+    // argument, so the branch is wave-uniform.  Heavy hitters +1.5%,
+    // Tuple<IntModN32 x 2> full domain +2.5% (profiles/r13_ab.txt).
+    uint32_t r = w[3] >= d.dn ? w[3] - d.dn : w[3];
+    q[2] = div_2by1(r, w[2], d.dn, d.v, r);
+    q[1] = div_2by1(r, w[1], d.dn, d.v, r);
+    q[0] = div_2by1(r, w[0], d.dn, d.v, r);
+    return r;
+  }
   const int sh = d.sh;
   uint32_t u4 = sh ? (w[3] >> (32 - sh)) : 0u;
   uint32_t u3 = (w[3] << sh) | (sh ? (w[2] >> (32 - sh)) : 0u);

@@ -113,6 +113,11 @@ CASES = [
     ([(7, ("intmodn", 64, G.M64), 48.0), (9, ("intmodn", 64, G.M64), 48.0)], [0, 1]),
     ([(4, ("intmodn", 32, G.M32), 48.0), (6, ("intmodn", 32, G.M32), 48.0),
       (8, ("intmodn", 32, G.M32), 48.0)], [0, 1, 2]),
+    # Moduli below 2^31: the Moller-Granlund division's normalisation shifts.
+    ([(5, ("tuple", [("intmodn", 32, 1000003)] * 2), 48.0),
+      (7, ("tuple", [("intmodn", 32, 1000003)] * 2), 48.0),
+      (9, ("tuple", [("intmodn", 32, 1000003)] * 2), 48.0)], [0, 1, 2]),
+    ([(4, ("intmodn", 32, 251), 48.0), (6, ("intmodn", 32, 251), 48.0)], [0, 1]),
 ]
 
 

@@ -170,6 +170,11 @@ SPECIALISED_TYPES = [
     ("tuple", [("intmodn", 32, 65537)] * 3),
     ("tuple", [("intmodn", 32, 4294967295)] * 2),
     ("tuple", [("intmodn", 32, M32)] * 4),
+    # Moduli below 2^31 (normalisation shifts in the Moller-Granlund division)
+    # and 2^31 itself, on the octet kernel's Mod32Leaf<2> and the single leaf.
+    ("tuple", [("intmodn", 32, 2147483647)] * 2),
+    ("intmodn", 32, 3),
+    ("tuple", [("intmodn", 32, 2147483648)] * 2),
 ]
 
 
@@ -189,7 +194,7 @@ def test_expand_specialised_leaves(hip, vt, party, sec):
 # 4 IntModN32 leaves use Mod32Leaf<4>, both on the pair kernel.
 EXPECTED_KERNEL = ["octet/fast", "pair/fast", "octet/swar", "octet/swar", "octet/swar",
                    "octet/swar", "octet/swar", "octet/mod32", "octet/mod32", "pair/mod32",
-                   "octet/mod32", "pair/mod32"]
+                   "octet/mod32", "pair/mod32", "octet/mod32", "octet/mod32", "octet/mod32"]
 
 
 @pytest.mark.parametrize("i", range(len(SPECIALISED_TYPES)),
