@@ -208,6 +208,7 @@ StatusOr<std::vector<uint8_t>> DistributedComparisonFunction::EvaluatePacked(
   // One key: its arrays and the points go through the reused scratch buffers
   // (staged, no per-call allocation), then one launch and one copy back.
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   const int64_t m = static_cast<int64_t>(xs.size());
   std::vector<dpf_block> pts(m);
   for (int64_t i = 0; i < m; ++i) pts[i] = ToBlock(xs[i]);

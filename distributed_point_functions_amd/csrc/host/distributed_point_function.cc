@@ -411,6 +411,7 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   // Everything that can fail on the host is checked before device work starts.
   if (before_device) DPF_RETURN_IF_ERROR(before_device());
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   std::vector<dpf_block> paths(std::max<int64_t>(n, 1));
   dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) paths[i] = ToBlock(prefixes[i]);
@@ -526,6 +527,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   // ExpandAndUpdateContext (cc:455-498): starting seeds on the device.  The
   // value correction of this level (h:761-780) is parsed before device work.
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   std::vector<uint128> vcw;
   auto parse_vcw = [&]() -> Status {
     DPF_ASSIGN_OR_RETURN(vcw, ValueCorrectionLeaves(ctx.key(), hierarchy_level));
@@ -680,6 +682,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
   if (!device_out || capacity_bytes < total * f.packed_size)
     return InvalidArgumentError("device output buffer too small");
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   // Walk the root to the shard's subtree root along the top k tree bits.
   dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
   uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
@@ -751,6 +754,7 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
     }
   }
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   const int stop_level = hierarchy_to_tree()[hierarchy_level];
   int start_level = 0;
   DeviceStart start;
@@ -841,6 +845,7 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtBatchPacked(
     if (E > 1) block_index[i] = static_cast<int32_t>(points[i] & ((static_cast<uint128>(1) << bib) - 1));
   }
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   DPF_RETURN_IF_ERROR(s->Upload(s->key_seed, seeds.data(), seeds.size()));
   DPF_RETURN_IF_ERROR(s->Upload(s->party, party.data(), party.size()));
   DPF_RETURN_IF_ERROR(s->Upload(s->cw_seed, cw_seed.data(), cw_seed.size()));

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <utility>
@@ -403,8 +404,13 @@ class StreamFence {
   void* last_stream_ = nullptr;
 };
 
+// The device buffers and staging of one DistributedPointFunction (or
+// DistributedComparisonFunction).  The reference's const evaluation methods
+// may be called from several threads at once; `mu` makes every call that
+// uses these buffers take them in turn (recursive: a call's helpers lock too).
 class DeviceScratch {
  public:
+  std::recursive_mutex mu;
   PackedUploads packed;
   DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
   DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;

@@ -382,6 +382,7 @@ Status DistributedPointFunction::EvaluateAtBatchSumToDevice(const DeviceKeyBatch
   if (bad) return InvalidArgumentError("`evaluation_points` larger than the domain size at hierarchy level " +
                                        std::to_string(hierarchy_level));
   auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   // The workspace is zeroed and accumulated into on `stream`: an earlier call
   // on another stream must have finished with it first (device-side wait).
   DPF_RETURN_IF_ERROR(s->workspace_fence.Acquire(
