@@ -26,6 +26,7 @@ def test_documented_scheduler_and_fence_settings():
     assert B.DEFAULT_SCHED_TUS == {"dpf_batch.hip"}
     # The fence every 2 last-round chains (aes_core.h default), none in the batch TU.
     assert B.fence_setting(os.path.join(KDIR, "dpf_kernels.hip")) == 2
+    assert B.fence_setting(os.path.join(KDIR, "dpf_dcf.hip")) == 2
     assert B.fence_setting(os.path.join(KDIR, "dpf_batch.hip")) == 1024
     src = open(os.path.join(KDIR, "aes_core.h")).read()
     assert re.search(r"sched_barrier\(0\)", src)
@@ -70,6 +71,8 @@ def test_compiler_crash_reports_known_issue_and_falls_back(tmp_path, monkeypatch
 def test_clean_build_records_settings(tmp_path, monkeypatch, capsys):
     man = _build_with(tmp_path, _fake_hipcc(tmp_path, crash_on_ilp=False), monkeypatch)
     assert man["dpf_kernels.hip"] == {"scheduler": "iterative-ilp", "last_round_fence": 2}
+    assert man["dpf_dcf.hip"] == {"scheduler": "iterative-ilp", "last_round_fence": 2}
+    assert man["dpf_batch.hip"] == {"scheduler": "default", "last_round_fence": 1024}
     assert "KNOWN ISSUE" not in capsys.readouterr().out
 
 
