@@ -11,6 +11,9 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <unordered_map>
@@ -460,6 +463,39 @@ StatusOr<int64_t> DistributedPointFunction::OutputElements(int hierarchy_level,
   return std::max<int64_t>(num_prefixes, 1) << (log - prev_log);
 }
 
+namespace {
+// Host-phase timing of EvaluateUntil, printed at exit when DPF_HOST_TIMING is
+// set: where a small call's microseconds go (validation, uploads, launch,
+// output copy).
+struct UntilTiming {
+  double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long calls = 0;
+  ~UntilTiming() {
+    const double n = static_cast<double>(calls - 100);
+    if (calls > 100 && std::getenv("DPF_HOST_TIMING"))
+      std::fprintf(stderr,
+                   "[EvaluateUntil host timing] calls=%ld per call: validate=%.2fus "
+                   "reset+vcw=%.2fus pack=%.2fus commit=%.2fus launch=%.2fus reserve=%.2fus "
+                   "copy=%.2fus\n",
+                   calls, t[0] * 1e6 / n, t[5] * 1e6 / n, t[6] * 1e6 / n, t[1] * 1e6 / n,
+                   t[2] * 1e6 / n, t[3] * 1e6 / n, t[4] * 1e6 / n);
+  }
+};
+UntilTiming g_until_timing;
+const bool g_until_timing_on = std::getenv("DPF_HOST_TIMING") != nullptr;
+struct UntilClock {
+  std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+  void mark(int phase) {
+    if (!g_until_timing_on) return;
+    auto now = std::chrono::steady_clock::now();
+    // The first 100 calls (allocations, page-locked buffers) are not counted.
+    if (g_until_timing.calls > 100)
+      g_until_timing.t[phase] += std::chrono::duration<double>(now - last).count();
+    last = now;
+  }
+};
+}  // namespace
+
 Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<const uint128> prefixes,
                                                    EvaluationContext& ctx,
                                                    const ValueType* requested_type,
@@ -467,6 +503,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
                                                    void* stream, const HostSink* host_out,
                                                    int64_t* num_elements) const {
   // h:641-837
+  UntilClock clk;
   DPF_RETURN_IF_ERROR(validator_->ValidateEvaluationContext(ctx));
   const int H = static_cast<int>(parameters().size());
   if (hierarchy_level < 0 || hierarchy_level >= H)
@@ -528,6 +565,8 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   // value correction of this level (h:761-780) is parsed before device work.
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
+  if (g_until_timing_on) ++g_until_timing.calls;
+  clk.mark(0);
   std::vector<uint128> vcw;
   auto parse_vcw = [&]() -> Status {
     DPF_ASSIGN_OR_RETURN(vcw, ValueCorrectionLeaves(ctx.key(), hierarchy_level));
@@ -564,10 +603,12 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   const int64_t total = num_prefixes == 0 ? corrected : num_prefixes * outputs_per_prefix;
   *num_elements = total;
 
+  clk.mark(5);
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
   const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());
   const PackedCws o_cw = AddCorrectionWords(ctx.key(), start_level, stop_level, up);
+  clk.mark(6);
   DPF_RETURN_IF_ERROR(up.Commit(stream));
   if (tree_indices.empty()) {
     start.seeds = up.Ptr<dpf_block>(o_root);
@@ -594,6 +635,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   }
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  clk.mark(1);
   HIP_RETURN_IF_ERROR(dpf_hip_expand(start.n, start.seeds, start.ctrl, L, up.Ptr<dpf_block>(o_cw.seed),
                                      up.Ptr<uint8_t>(o_cw.left), up.Ptr<uint8_t>(o_cw.right), &kl, &kr,
                                      &kv, &desc, cepb, up.Ptr<dpf_block>(o_vcw),
@@ -616,10 +658,13 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     HIP_RETURN_IF_ERROR(dpf_hip_gather(num_prefixes, outputs_per_prefix, esz,
                                        s->offsets.as<int64_t>(), expand_out, result, stream));
   }
+  clk.mark(2);
   if (!device_out) {
     const size_t bytes = static_cast<size_t>(total) * esz;
     void* dst = host_out->reserve(bytes);
+    clk.mark(3);
     HIP_RETURN_IF_ERROR(CopyToHostSink(*host_out, dst, result, bytes, stream));
+    clk.mark(4);
   }
   return OkStatus();
 }

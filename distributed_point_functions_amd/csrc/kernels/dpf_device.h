@@ -66,14 +66,28 @@ struct LdsImage {
 // reads copy (l & 31), so every ds_read_b32 of a wave is bank-conflict-free.
 // Filled 16 bytes (4 copies) per store: 8192 ds_write_b128 per workgroup, so a
 // small workgroup (block_for) fills its tables in a few microseconds.
+// The T0 loads of 16 stores are issued together: a 64-thread workgroup (small
+// launches, block_for) makes 128 stores per thread, and one dependent
+// constant-memory load per store cost ~40 us of a 2^12-output EvaluateUntil.
 __device__ __forceinline__ void fill_tables(uint32_t* tab) {
-  for (int q = threadIdx.x; q < kTabWords / 4; q += blockDim.x) {
-    // q = (entry e, table t, quad k): words [half * 16384 + e * 64 + (t & 1) * 32 + 4k, +4)
-    const int e = q >> 5, t = (q >> 3) & 3, k = q & 7;
-    const uint32_t v0 = c_t0.v[e];
-    const uint32_t v = t == 0 ? v0 : ((v0 << (8 * t)) | (v0 >> (32 - 8 * t)));
-    *reinterpret_cast<uint4*>(tab + (t >> 1) * 16384 + e * 64 + (t & 1) * 32 + 4 * k) =
-        make_uint4(v, v, v, v);
+  constexpr int kQuads = kTabWords / 4, kBatch = 16;
+  for (int q0 = threadIdx.x; q0 < kQuads; q0 += kBatch * blockDim.x) {
+    uint32_t v0[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int q = q0 + j * blockDim.x;
+      v0[j] = q < kQuads ? c_t0.v[q >> 5] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      // q = (entry e, table t, quad k): words [half * 16384 + e * 64 + (t & 1) * 32 + 4k, +4)
+      const int q = q0 + j * blockDim.x;
+      if (q >= kQuads) break;
+      const int e = q >> 5, t = (q >> 3) & 3, k = q & 7;
+      const uint32_t v = t == 0 ? v0[j] : ((v0[j] << (8 * t)) | (v0[j] >> (32 - 8 * t)));
+      *reinterpret_cast<uint4*>(tab + (t >> 1) * 16384 + e * 64 + (t & 1) * 32 + 4 * k) =
+          make_uint4(v, v, v, v);
+    }
   }
 }
 
