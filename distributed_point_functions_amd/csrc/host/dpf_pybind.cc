@@ -73,7 +73,6 @@ py::array_t<uint8_t> ToArray(std::vector<uint8_t>&& v) {
   return py::array_t<uint8_t>({static_cast<py::ssize_t>(owned->size())}, {py::ssize_t{1}},
                               owned->data(), free_when_done);
 }
-py::array_t<uint8_t> ToArray(const std::vector<uint8_t>& v) { return ToArray(std::vector<uint8_t>(v)); }
 
 std::unique_ptr<ValueType> OptType(const py::object& o) {
   if (o.is_none()) return nullptr;
