@@ -107,6 +107,7 @@ struct PyBatchContext {
   std::shared_ptr<DeviceBatchContext> ctx;
   int PreviousHierarchyLevel() const { return ctx->previous_hierarchy_level(); }
   int PartialEvaluationsLevel() const { return ctx->partial_evaluations_level(); }
+  int ExpansionCacheLevel() const { return ctx->expansion_cache_level(); }
   int64_t NumPartialEvaluations() const {
     return static_cast<int64_t>(ctx->partial_prefixes().size());
   }
@@ -454,6 +455,7 @@ PYBIND11_MODULE(_dpf_host, m) {
   py::class_<PyBatchContext>(m, "DeviceBatchContext")
       .def_property_readonly("previous_hierarchy_level", &PyBatchContext::PreviousHierarchyLevel)
       .def_property_readonly("partial_evaluations_level", &PyBatchContext::PartialEvaluationsLevel)
+      .def_property_readonly("expansion_cache_level", &PyBatchContext::ExpansionCacheLevel)
       .def_property_readonly("num_partial_evaluations", &PyBatchContext::NumPartialEvaluations)
       .def("reset", [](PyBatchContext& c) { c.ctx->Reset(); });
   py::class_<PyKeyBatch>(m, "KeyBatch")

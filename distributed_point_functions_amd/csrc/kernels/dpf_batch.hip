@@ -78,6 +78,12 @@ struct BatchLevelParams {
   int64_t out_row;          // STORE: bytes per key row
   char* out;
   unsigned long long* wide;  // SUM: [slot][leaf][3]
+  // Expansion cache (optional): every tree leaf of this call, [key][u << E + l],
+  // the start nodes of the next level's call (no path re-derivation).  A
+  // non-root node's seed has bit 0 clear (distributed_point_function.cc:
+  // 323-343), so the cache keeps the control bit there: one 16-byte store.
+  dpf_block* leaf_seeds;
+  int64_t leaf_stride;
   RoundKeys rkl, rkr, rkd, rkv;
 };
 
@@ -354,7 +360,7 @@ struct GenericV {
 template <int MAXE, class V, class Sink>
 __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const BatchLevelParams& p,
                                                    const V& v, int64_t k, Block4 node,
-                                                   uint32_t t, Sink&& sink) {
+                                                   uint32_t t, int64_t leaf_at, Sink&& sink) {
   Block4 N[1 << MAXE];
   uint32_t T = 0;  // bit i = control bit of N[i]
   N[0] = node;
@@ -391,6 +397,18 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
           T = (T & ~(15u << (2 * i - 2))) | (t[2] << (2 * i - 2)) | (t[3] << (2 * i - 1)) |
               (t[0] << (2 * i)) | (t[1] << (2 * i + 1));
         }
+      }
+    }
+  }
+  // The expansion cache: this start node's 2^E leaves (node and control bit),
+  // 2^E consecutive entries per lane.
+  if (leaf_at >= 0) {
+#pragma unroll
+    for (int i = 0; i < (1 << MAXE); ++i) {
+      if (i < (1 << E)) {
+        Block4 c = N[i];
+        c.w0 |= (T >> i) & 1u;
+        store_block(p.leaf_seeds + leaf_at + i, c);
       }
     }
   }
@@ -484,15 +502,19 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
         vk.key(p, k);
         const Block4 node = which ? sb : sa;
         const uint32_t tn = which ? tb : ta;
+        const int64_t leaf_at =
+            p.leaf_seeds && valid ? k * p.leaf_stride + (u << p.expand_levels) : -1;
         if constexpr (SUM) {
-          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, [&](int l, const typename V::Val& val) {
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_at,
+                                   [&](int l, const typename V::Val& val) {
 #pragma unroll
             for (int i = 0; i < (1 << MAXE); ++i)
               if (i == l) vk.acc_add(acc[i], val);
           });
         } else {
           char* row = p.out + k * p.out_row + (u << p.expand_levels) * (int64_t)p.epl * p.esz;
-          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, [&](int l, const typename V::Val& val) {
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_at,
+                                   [&](int l, const typename V::Val& val) {
             if (valid) vk.store(lk, p, row + (int64_t)l * p.epl * p.esz, val);
           });
         }
@@ -537,6 +559,23 @@ __global__ void sum_rows_kernel(int64_t rows, int64_t row_len, dpf_value_desc d,
       GenericLeaf::store_le(o, acc[k], lb);
       o += lb;
     }
+  }
+}
+
+// Start seeds of a call from the previous call's expansion cache:
+// seeds_out[k*T + i] = cache[k*cache_stride + slot[i]] (and the control bits).
+__global__ void gather_seeds_kernel(int64_t keys, int64_t T, const int64_t* __restrict__ slot,
+                                    const dpf_block* __restrict__ cache, int64_t cache_stride,
+                                    dpf_block* __restrict__ seeds_out,
+                                    uint8_t* __restrict__ ctrl_out) {
+  const int64_t total = keys * T;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = x / T, i = x - k * T;
+    Block4 c = load_block(cache + k * cache_stride + slot[i]);
+    ctrl_out[x] = (uint8_t)(c.w0 & 1u);
+    c.w0 &= ~1u;
+    store_block(seeds_out + x, c);
   }
 }
 
@@ -611,6 +650,38 @@ int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_lev
                               const dpf_aes_key* key_value, const dpf_value_desc* desc,
                               int elements_per_leaf, const dpf_block* value_correction, int sum,
                               uint64_t* workspace, void* out, void* stream) {
+  return dpf_hip_eval_prefix_batch_cached(
+      num_keys, num_starts, walk_levels, save_after, expand_levels, cw_first, cw_stride, key_seed,
+      party, seeds_in, control_in, in_stride, parent, path, save_index, seeds_out, control_out,
+      out_stride, cw_seed, cw_left, cw_right, key_left, key_right, key_value, desc,
+      elements_per_leaf, value_correction, sum, workspace, out, nullptr, 0, stream);
+}
+
+int dpf_hip_gather_seeds(int64_t num_keys, int64_t num_rows, const int64_t* slot,
+                         const dpf_block* cache, int64_t cache_stride, dpf_block* seeds_out,
+                         uint8_t* control_out, void* stream) {
+  if (num_keys < 0 || num_rows < 0 || cache_stride < 0) return fail(kInvalidArgument, "bad sizes");
+  const int64_t total = num_keys * num_rows;
+  if (total == 0) return kOk;
+  if (!slot || !cache || !seeds_out || !control_out) return fail(kInvalidArgument, "NULL pointer");
+  int64_t g = (total + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(gather_seeds_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+                     num_keys, num_rows, slot, cache, cache_stride, seeds_out, control_out);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+int dpf_hip_eval_prefix_batch_cached(
+    int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
+    int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
+    const dpf_block* seeds_in, const uint8_t* control_in, int64_t in_stride,
+    const int32_t* parent, const dpf_block* path, const int32_t* save_index, dpf_block* seeds_out,
+    uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed, const uint8_t* cw_left,
+    const uint8_t* cw_right, const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+    const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
+    const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
+    dpf_block* leaf_cache, int64_t leaf_stride, void* stream) {
   int st = validate_desc(desc);
   if (st) return st;
   const int max_e = dpf_hip_prefix_batch_max_expand(desc, sum);
@@ -676,6 +747,12 @@ int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_lev
     p.out_row = slots * p.esz;
     p.out = (char*)out;
     p.wide = reinterpret_cast<unsigned long long*>(workspace);
+    if (leaf_cache) {
+      if (leaf_stride < (num_starts << expand_levels))
+        return fail(kInvalidArgument, "expansion cache too small");
+      p.leaf_seeds = leaf_cache;
+      p.leaf_stride = leaf_stride;
+    }
     p.rkl = expand_key(key_left);
     p.rkr = expand_key(key_right);
     p.rkv = expand_key(key_value);

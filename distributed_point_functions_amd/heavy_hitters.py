@@ -169,11 +169,13 @@ def verify(record, logs: Sequence[int], values: np.ndarray, idx: np.ndarray) -> 
                                      f"({c}, {t}), plaintext count {want}")
 
 
-def algorithmic_aes(dpf, logs: Sequence[int], record, num_keys: int) -> int:
+def algorithmic_aes(dpf, logs: Sequence[int], record, num_keys: int, walk: bool = True) -> int:
     """AES blocks one server spends per pass: per level with P
     prefixes, P*(D_p - D_pp) path steps (from the root at the second level) +
     2*P*(2^(D_h - D_p) - 1) expansion + b*P*2^(D_h - D_p) value hashes, with
-    b = 2 blocks read by the sampling; the first level is a full expansion."""
+    b = 2 blocks read by the sampling; the first level is a full expansion.
+    walk=False: the device context's expansion cache supplies every level's
+    tree nodes, so the path steps are not computed."""
     h2t = dpf.hierarchy_to_tree()
     total = 0
     for h, vals, _, _ in record:
@@ -183,6 +185,6 @@ def algorithmic_aes(dpf, logs: Sequence[int], record, num_keys: int) -> int:
             continue
         p = len(vals) >> (logs[h] - logs[h - 1])
         d_p = h2t[h - 1]
-        walk = d_p - (h2t[h - 2] if h >= 2 else 0)
-        total += p * walk + 2 * p * ((1 << (d_h - d_p)) - 1) + 2 * p * (1 << (d_h - d_p))
+        steps = d_p - (h2t[h - 2] if h >= 2 else 0) if walk else 0
+        total += p * steps + 2 * p * ((1 << (d_h - d_p)) - 1) + 2 * p * (1 << (d_h - d_p))
     return total * num_keys

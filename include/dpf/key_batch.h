@@ -109,7 +109,10 @@ class DeviceBatchContext {
     previous_hierarchy_level_ = -1;
     partial_evaluations_level_ = -1;
     partial_prefixes_.clear();
+    leaf_level_ = -1;
   }
+  // Hierarchy level whose call wrote the expansion cache (-1: none).
+  int expansion_cache_level() const { return leaf_level_; }
 
  private:
   friend class DistributedPointFunction;
@@ -128,6 +131,18 @@ class DeviceBatchContext {
   void* next_seeds_ = nullptr;  // written by the next evaluation, then swapped in
   void* next_ctrl_ = nullptr;
   size_t next_seeds_cap_ = 0, next_ctrl_cap_ = 0;
+  // Expansion cache: the tree leaves of the last call ([key][leaf_stride_]),
+  // i.e. the next call's tree nodes (DistributedPointFunction's batched
+  // EvaluateUntil gathers its start seeds from it instead of walking down
+  // from the partial evaluations two calls back).  leaf_de_: levels from a
+  // tree index of that call to its leaves.
+  void* leaf_seeds_ = nullptr;  // seed | control bit (bit 0)
+  size_t leaf_seeds_cap_ = 0;
+  int64_t leaf_stride_ = 0;
+  int leaf_level_ = -1;
+  int leaf_de_ = 0;
+  void* slots_ = nullptr;
+  size_t slots_cap_ = 0;
   // Per-call scratch: start-node tables, sums workspace, staging output.
   void* parent_ = nullptr;
   void* path_ = nullptr;

@@ -273,6 +273,33 @@ int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_lev
                               int elements_per_leaf, const dpf_block* value_correction, int sum,
                               uint64_t* workspace, void* out, void* stream);
 
+/* dpf_hip_eval_prefix_batch that also writes the expansion cache: every tree
+ * leaf of the call (2^expand_levels per start node u) to
+ * leaf_cache[k*leaf_stride + (u << expand_levels) + l] (leaf_stride >=
+ * num_starts << expand_levels), the node's seed with its control bit in bit 0
+ * (clear in every non-root seed).  The next level's tree nodes are among these
+ * leaves, so its start seeds are gathered from them (dpf_hip_gather_seeds)
+ * instead of re-derived by a path walk from the partial evaluations two calls
+ * back (distributed_point_function.cc:351-453).  The
+ * leaves must not be the root (depth > 0).  leaf_cache == NULL: no cache. */
+int dpf_hip_eval_prefix_batch_cached(
+    int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
+    int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
+    const dpf_block* seeds_in, const uint8_t* control_in, int64_t in_stride,
+    const int32_t* parent, const dpf_block* path, const int32_t* save_index, dpf_block* seeds_out,
+    uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed, const uint8_t* cw_left,
+    const uint8_t* cw_right, const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+    const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
+    const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
+    dpf_block* leaf_cache, int64_t leaf_stride, void* stream);
+
+/* seeds_out[k*num_rows + i] / control_out[k*num_rows + i] = the seed (bit 0
+ * cleared) and control bit (bit 0) of cache[k*cache_stride + slot[i]]: a
+ * call's start seeds from the previous call's expansion cache. */
+int dpf_hip_gather_seeds(int64_t num_keys, int64_t num_rows, const int64_t* slot,
+                         const dpf_block* cache, int64_t cache_stride, dpf_block* seeds_out,
+                         uint8_t* control_out, void* stream);
+
 /* Largest expand_levels dpf_hip_eval_prefix_batch accepts for this value type
  * (register-resident subtree), or -1 if `sum` mode is not available. */
 int dpf_hip_prefix_batch_max_expand(const dpf_value_desc* desc, int sum);

@@ -7,6 +7,8 @@ outputs must equal the CPU oracle's EvaluateUntil
 the summed variant must equal the group sum of those outputs, and the exported
 per-key context must equal the oracle's context after the same calls.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -51,12 +53,24 @@ def _prefix_plan(P, plan, rng, first_prefix_count=6):
     return out
 
 
+def _check_export(dpf, bctx, batch, octx, k):
+    """Lazy export of the device context == the oracle's per-key context."""
+    ctx = dpf.export_evaluation_context(bctx, batch, k)
+    assert ctx.previous_hierarchy_level == octx[k]["prev"]
+    got = [(D.u128_from_block(e.prefix), D.u128_from_block(e.seed), int(e.control_bit))
+           for e in ctx.partial_evaluations]
+    assert sorted(got) == sorted(set(octx[k]["partials"]))
+    if octx[k]["partials"]:
+        assert ctx.partial_evaluations_level == octx[k]["partials_level"]
+
+
 def _run(levels, plan, n_keys, sum_mode, seed, party_mix=True):
     import torch
     dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=seed, party_mix=party_mix)
     dev = dpf.upload_key_batch(batch)
     bctx = dpf.create_batch_evaluation_context(dev)
     octx = [O.create_context(P, k) for k in oks]
+    cache_on = os.environ.get("DPF_BATCH_NO_CACHE") != "1"
     for h, prefixes in _prefix_plan(P, plan, rng):
         size = dpf.packed_size(h)
         vt = levels[h][1]
@@ -77,15 +91,13 @@ def _run(levels, plan, n_keys, sum_mode, seed, party_mix=True):
             for k in range(n_keys):
                 np.testing.assert_array_equal(got[k], want[k], err_msg=f"level {h} key {k}")
         assert bctx.previous_hierarchy_level == h
-    # Lazy export of the device context == the oracle's per-key context.
+        # The expansion cache is written by every call but the last level's
+        # (and not when the level's leaves are the root: tree depth 0).
+        writes = cache_on and h < len(levels) - 1 and dpf.hierarchy_to_tree()[h] > 0
+        assert bctx.expansion_cache_level == (h if writes else -1)
+        _check_export(dpf, bctx, batch, octx, n_keys - 1)
     for k in (0, n_keys - 1):
-        ctx = dpf.export_evaluation_context(bctx, batch, k)
-        assert ctx.previous_hierarchy_level == octx[k]["prev"]
-        got = [(D.u128_from_block(e.prefix), D.u128_from_block(e.seed), int(e.control_bit))
-               for e in ctx.partial_evaluations]
-        assert sorted(got) == sorted(set(octx[k]["partials"]))
-        if octx[k]["partials"]:
-            assert ctx.partial_evaluations_level == octx[k]["partials_level"]
+        _check_export(dpf, bctx, batch, octx, k)
     return dpf, bctx
 
 
@@ -131,6 +143,16 @@ def test_batch_incremental_per_key(levels, plan, n_keys):
 @pytest.mark.parametrize("n_keys", [3, 130])
 def test_batch_incremental_sum(levels, plan, n_keys):
     _run(levels, plan, n_keys, True, seed=n_keys * 5 + len(levels))
+
+
+@pytest.mark.parametrize("levels,plan", CASES[:4] + CASES[-3:], ids=lambda x: str(x)[:60])
+@pytest.mark.parametrize("sum_mode", [False, True])
+def test_batch_incremental_without_expansion_cache(levels, plan, sum_mode, monkeypatch):
+    """DPF_BATCH_NO_CACHE=1: every call re-derives its tree nodes by the path
+    walk from the partial evaluations (the reference's ComputePartialEvaluations,
+    distributed_point_function.cc:351-453) -- same outputs and contexts."""
+    monkeypatch.setenv("DPF_BATCH_NO_CACHE", "1")
+    _run(levels, plan, 37, sum_mode, seed=len(levels) + 11)
 
 
 def test_batch_many_prefixes_one_key():
