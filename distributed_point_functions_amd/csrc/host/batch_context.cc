@@ -63,6 +63,12 @@ bool CacheOn() {
   const char* v = std::getenv("DPF_BATCH_NO_CACHE");
   return !(v && v[0] == '1');
 }
+// DPF_BATCH_CACHE_IN_PLACE=1 acts as if no spare cache buffer fitted (gather
+// the start seeds, rewrite the cache in place): a test hook for that path.
+bool SpareOff() {
+  const char* v = std::getenv("DPF_BATCH_CACHE_IN_PLACE");
+  return v && v[0] == '1';
+}
 struct PhaseClock {
   std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
   void mark(int phase) {
@@ -86,7 +92,7 @@ Status DeviceBatchContext::Ensure(void** p, size_t* cap, size_t bytes) {
 
 DeviceBatchContext::~DeviceBatchContext() {
   for (void* p : {seeds_, ctrl_, next_seeds_, next_ctrl_, parent_, path_, save_, offsets_,
-                  workspace_, stage_, stage2_, leaf_seeds_, slots_})
+                  workspace_, stage_, stage2_, leaf_seeds_, leaf_spare_, slots_})
     if (p) dpf_hip_free(p);
 }
 
@@ -252,12 +258,12 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   const int64_t K = keys.num_keys();
   // The previous call's expansion cache holds this call's tree nodes (its
   // leaves are the children, W1 levels down, of the tree indices the
-  // partial evaluations stand for): their seeds are gathered from it and the
-  // W1-level path walk is skipped.  Outputs and the
+  // partial evaluations stand for): the kernel reads their seeds from it and
+  // the W1-level path walk is skipped.  Outputs and the
   // partial evaluations are the same either way.
   const bool g_cache_on = CacheOn();
   const bool cached = g_cache_on && P > 0 && ctx.leaf_seeds_ && ctx.leaf_level_ == prev &&
-                      ctx.leaf_de_ == W1;
+                      ctx.leaf_de_ == W1 && ctx.leaf_stride_ <= INT32_MAX;
   const int Wk = cached ? 0 : W1;  // levels walked above each tree index
   const int cepb = corrected_elements_per_block(hierarchy_level);
   const int esz = f.packed_size;
@@ -271,6 +277,46 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   const int64_t need = (sum ? n : K * n) * esz;
   if (!device_out || capacity_bytes < need) return InvalidArgumentError("device output buffer too small");
   const bool update_ctx = P > 0 && hierarchy_level < H - 1;
+
+  // This call's leaves become the next call's expansion cache (not after the
+  // last level).  Preferred: write them to the spare buffer while the kernel
+  // reads the start seeds straight from the current cache, then swap.  With
+  // no room for a spare, the start seeds are gathered first and the current
+  // cache is rewritten in place; a failed allocation only turns the cache off.
+  const int64_t leaf_stride = U << E;
+  void* leaf_seeds = nullptr;
+  bool swap_cache = false;
+  bool gather = false;
+  if (g_cache_on && hierarchy_level < H - 1 && Dh > 0) {
+    const size_t cache_need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
+    if (!cached) {
+      // The current cache is not read by this call: rewrite (or regrow) it.
+      if (ctx.leaf_seeds_cap_ < cache_need) {
+        HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+        if (ctx.leaf_seeds_) dpf_hip_free(ctx.leaf_seeds_);
+        ctx.leaf_seeds_cap_ = 0;
+        if (dpf_hip_alloc(&ctx.leaf_seeds_, cache_need) == 0) ctx.leaf_seeds_cap_ = cache_need;
+      }
+      leaf_seeds = ctx.leaf_seeds_;
+    } else {
+      if (SpareOff()) {
+        // test hook: no spare
+      } else if (ctx.leaf_spare_cap_ < cache_need) {
+        // The spare may still be read by work in flight on the stream.
+        HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+        if (ctx.leaf_spare_) dpf_hip_free(ctx.leaf_spare_);
+        ctx.leaf_spare_cap_ = 0;
+        if (dpf_hip_alloc(&ctx.leaf_spare_, cache_need) == 0) ctx.leaf_spare_cap_ = cache_need;
+      }
+      if (ctx.leaf_spare_ && ctx.leaf_spare_cap_ >= cache_need && !SpareOff()) {
+        leaf_seeds = ctx.leaf_spare_;
+        swap_cache = true;
+      } else {
+        gather = true;  // leaf_seeds is set once the gather is enqueued
+      }
+    }
+  }
+  const bool direct = cached && !gather;  // start seeds read from the cache
 
   clk.mark(1);
   // Start-node tables: u = tree index i * 2^s + sub.  Host staging buffers
@@ -288,19 +334,24 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     path.resize(U);
   }
   const uint128 w1_mask = Wk >= 128 ? ~uint128{0} : ((uint128{1} << Wk) - 1);
+  const uint128 leaf_mask = cached ? (uint128{1} << W1) - 1 : 0;  // W1 <= 62 when cached
   static thread_local std::vector<int64_t> tl_slots;
   std::vector<int64_t>& slots = tl_slots;
-  if (cached) slots.resize(T);
-  const uint128 leaf_mask = cached ? (uint128{1} << W1) - 1 : 0;  // W1 <= 62 when cached
+  if (gather) slots.resize(T);
   dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
       const uint128 low = tree_indices[i] & w1_mask;
-      if (cached)
-        slots[i] = (static_cast<int64_t>(from_root ? 0 : parent_of[i]) << W1) |
-                   static_cast<int64_t>(tree_indices[i] & leaf_mask);
+      // Cached: the cache slot of tree index i (its parent's leaf row).
+      const int64_t slot = cached ? (static_cast<int64_t>(from_root ? 0 : parent_of[i]) << W1) |
+                                        static_cast<int64_t>(tree_indices[i] & leaf_mask)
+                                  : 0;
+      if (gather) slots[i] = slot;
+      const int32_t start = direct ? static_cast<int32_t>(slot)
+                            : gather ? static_cast<int32_t>(i)
+                                     : (from_root ? 0 : parent_of[i]);
       for (int64_t sub = 0; sub < (int64_t{1} << s); ++sub) {
         const int64_t u = (i << s) + sub;
-        parent[u] = cached ? static_cast<int32_t>(i) : (from_root ? 0 : parent_of[i]);
+        parent[u] = start;
         path[u] = ToBlock(s ? ((low << s) | static_cast<uint128>(sub)) : low);
         save[u] = sub == 0 ? static_cast<int32_t>(i) : -1;
       }
@@ -313,36 +364,29 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.parent_, parent.data(), U * sizeof(int32_t), stream));
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.path_, path.data(), U * sizeof(dpf_block), stream));
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.save_, save.data(), U * sizeof(int32_t), stream));
-  if (update_ctx || cached) {
+  if (update_ctx || gather) {
     DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.next_seeds_, &ctx.next_seeds_cap_,
                                                    K * T * sizeof(dpf_block)));
     DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.next_ctrl_, &ctx.next_ctrl_cap_, K * T));
   }
-  if (cached) {
-    // The start seeds (and, with update_ctx, the new partial evaluations).
+  if (gather) {
+    // The start seeds (and, with update_ctx, the new partial evaluations),
+    // read before the kernel rewrites the cache.
     DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.slots_, &ctx.slots_cap_, T * sizeof(int64_t)));
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.slots_, slots.data(), T * sizeof(int64_t), stream));
     HIP_RETURN_IF_ERROR(dpf_hip_gather_seeds(
         K, T, static_cast<const int64_t*>(ctx.slots_), static_cast<const dpf_block*>(ctx.leaf_seeds_),
         ctx.leaf_stride_, static_cast<dpf_block*>(ctx.next_seeds_),
         static_cast<uint8_t*>(ctx.next_ctrl_), stream));
-  }
-  // This call's leaves become the next call's expansion cache (not after the
-  // last level).  The cache buffers are rewritten in place (the gather above
-  // runs first on the stream); a larger cache is allocated beside the old one,
-  // and a failed allocation only turns the cache off.
-  const int64_t leaf_stride = U << E;
-  void* leaf_seeds = nullptr;
-  bool fresh_leaf = false;
-  if (g_cache_on && hierarchy_level < H - 1 && Dh > 0) {
-    const size_t need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
-    if (ctx.leaf_seeds_ && ctx.leaf_seeds_cap_ >= need) {
-      leaf_seeds = ctx.leaf_seeds_;
-    } else if (dpf_hip_alloc(&leaf_seeds, need) == 0) {
-      fresh_leaf = true;
-    } else {
-      leaf_seeds = nullptr;  // out of device memory: no cache, the next call walks
+    const size_t cache_need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
+    if (ctx.leaf_seeds_cap_ < cache_need) {
+      // Regrow once the gather has read the old cache.
+      HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+      dpf_hip_free(ctx.leaf_seeds_);
+      ctx.leaf_seeds_cap_ = 0;
+      if (dpf_hip_alloc(&ctx.leaf_seeds_, cache_need) == 0) ctx.leaf_seeds_cap_ = cache_need;
     }
+    leaf_seeds = ctx.leaf_seeds_;
   }
   std::vector<int64_t> offsets;
   if (!identity) {
@@ -356,14 +400,20 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
 
   clk.mark(3);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  // Cached start seeds carry their control bit in bit 0 (control_in NULL).
   const dpf_block* start_seeds =
-      cached ? static_cast<const dpf_block*>(ctx.next_seeds_) : (from_root ? nullptr : ctx.partial_seeds());
-  const uint8_t* start_ctrl =
-      cached ? static_cast<const uint8_t*>(ctx.next_ctrl_) : (from_root ? nullptr : ctx.partial_control());
-  const int64_t start_stride = cached ? T : static_cast<int64_t>(ctx.partial_prefixes_.size());
+      direct   ? static_cast<const dpf_block*>(ctx.leaf_seeds_)
+      : gather ? static_cast<const dpf_block*>(ctx.next_seeds_)
+               : (from_root ? nullptr : ctx.partial_seeds());
+  const uint8_t* start_ctrl = direct   ? nullptr
+                              : gather ? static_cast<const uint8_t*>(ctx.next_ctrl_)
+                                       : (from_root ? nullptr : ctx.partial_control());
+  const int64_t start_stride = direct   ? ctx.leaf_stride_
+                               : gather ? T
+                                        : static_cast<int64_t>(ctx.partial_prefixes_.size());
   auto launch = [&](int sum_mode, void* out, uint64_t* workspace) {
     return FromHip(dpf_hip_eval_prefix_batch_cached(
-        K, U, Wk + s, update_ctx && !cached ? W1 : -1, E, cached ? Dprev : start_level,
+        K, U, Wk + s, update_ctx && !gather ? Wk : -1, E, cached ? Dprev : start_level,
         keys.num_levels(), keys.seed(), keys.party(), start_seeds, start_ctrl, start_stride,
         static_cast<const int32_t*>(ctx.parent_), static_cast<const dpf_block*>(ctx.path_),
         static_cast<const int32_t*>(ctx.save_), static_cast<dpf_block*>(ctx.next_seeds_),
@@ -410,12 +460,9 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
                                                  ctx.stage_, device_out, stream));
   }
 
-  if (fresh_leaf) {
-    // The old cache (read by the gather) is released once the stream is past it.
-    HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
-    if (ctx.leaf_seeds_) dpf_hip_free(ctx.leaf_seeds_);
-    ctx.leaf_seeds_ = leaf_seeds;
-    ctx.leaf_seeds_cap_ = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
+  if (swap_cache) {
+    std::swap(ctx.leaf_seeds_, ctx.leaf_spare_);
+    std::swap(ctx.leaf_seeds_cap_, ctx.leaf_spare_cap_);
   }
   ctx.leaf_level_ = leaf_seeds ? hierarchy_level : -1;
   ctx.leaf_de_ = dE;

@@ -461,9 +461,17 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
       uint32_t ta, tb;
       if (p.seeds_in) {
         sa = load_block(p.seeds_in + ka * p.in_stride + par);
-        ta = p.ctrl_in[ka * p.in_stride + par] & 1u;
         sb = load_block(p.seeds_in + kb * p.in_stride + par);
-        tb = p.ctrl_in[kb * p.in_stride + par] & 1u;
+        if (p.ctrl_in) {
+          ta = p.ctrl_in[ka * p.in_stride + par] & 1u;
+          tb = p.ctrl_in[kb * p.in_stride + par] & 1u;
+        } else {
+          // Expansion cache layout: the control bit rides in bit 0 of the seed.
+          ta = sa.w0 & 1u;
+          tb = sb.w0 & 1u;
+          sa.w0 &= ~1u;
+          sb.w0 &= ~1u;
+        }
       } else {
         sa = load_block(p.key_seed + ka);
         ta = p.party[ka] & 1u;
@@ -568,14 +576,16 @@ __global__ void gather_seeds_kernel(int64_t keys, int64_t T, const int64_t* __re
                                     const dpf_block* __restrict__ cache, int64_t cache_stride,
                                     dpf_block* __restrict__ seeds_out,
                                     uint8_t* __restrict__ ctrl_out) {
-  const int64_t total = keys * T;
-  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
-       x += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = x / T, i = x - k * T;
-    Block4 c = load_block(cache + k * cache_stride + slot[i]);
-    ctrl_out[x] = (uint8_t)(c.w0 & 1u);
-    c.w0 &= ~1u;
-    store_block(seeds_out + x, c);
+  // blockIdx.y walks the keys, blockIdx.x the rows: no division per element.
+  for (int64_t k = blockIdx.y; k < keys; k += gridDim.y) {
+    const dpf_block* row = cache + k * cache_stride;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < T;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      Block4 c = load_block(row + slot[i]);
+      ctrl_out[k * T + i] = (uint8_t)(c.w0 & 1u);
+      c.w0 &= ~1u;
+      store_block(seeds_out + k * T + i, c);
+    }
   }
 }
 
@@ -664,9 +674,12 @@ int dpf_hip_gather_seeds(int64_t num_keys, int64_t num_rows, const int64_t* slot
   const int64_t total = num_keys * num_rows;
   if (total == 0) return kOk;
   if (!slot || !cache || !seeds_out || !control_out) return fail(kInvalidArgument, "NULL pointer");
-  int64_t g = (total + 255) / 256;
-  if (g > 65536) g = 65536;
-  hipLaunchKernelGGL(gather_seeds_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+  int64_t gx = (num_rows + 255) / 256;
+  if (gx > 64) gx = 64;
+  int64_t gy = num_keys < 65535 ? num_keys : 65535;
+  if (gx * gy > 262144) gy = (262144 + gx - 1) / gx;
+  hipLaunchKernelGGL(gather_seeds_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0,
+                     (hipStream_t)stream,
                      num_keys, num_rows, slot, cache, cache_stride, seeds_out, control_out);
   HIP_TRY(hipGetLastError());
   return kOk;
@@ -703,7 +716,7 @@ int dpf_hip_eval_prefix_batch_cached(
   }
   if (num_keys > 0 && num_starts > 0) {
     if (!party || !value_correction || !key_left || !key_right || !key_value ||
-        (!sum && !out) || (!seeds_in && !key_seed) || (seeds_in && (!control_in || !parent)) ||
+        (!sum && !out) || (!seeds_in && !key_seed) || (seeds_in && !parent) ||
         (walk_levels > 0 && !path) || (save_after >= 0 && (!seeds_out || !control_out || !save_index)) ||
         (walk_levels + expand_levels > 0 && (!cw_seed || !cw_left || !cw_right)))
       return fail(kInvalidArgument, "NULL pointer");
@@ -750,6 +763,9 @@ int dpf_hip_eval_prefix_batch_cached(
     if (leaf_cache) {
       if (leaf_stride < (num_starts << expand_levels))
         return fail(kInvalidArgument, "expansion cache too small");
+      if (seeds_in && (const void*)leaf_cache < (const void*)(seeds_in + num_keys * in_stride) &&
+          (const void*)seeds_in < (const void*)(leaf_cache + num_keys * leaf_stride))
+        return fail(kInvalidArgument, "expansion cache overlaps the start seeds");
       p.leaf_seeds = leaf_cache;
       p.leaf_stride = leaf_stride;
     }

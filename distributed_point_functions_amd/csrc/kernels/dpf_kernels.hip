@@ -890,7 +890,12 @@ int dpf_hip_alloc(void** ptr, size_t bytes) {
   if (!ptr) return fail(kInvalidArgument, "ptr is NULL");
   *ptr = nullptr;
   if (bytes == 0) bytes = 1;
-  HIP_TRY(hipMalloc(ptr, bytes));
+  const hipError_t e = hipMalloc(ptr, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // an allocation failure must not fail the next launch check
+    *ptr = nullptr;
+  }
+  HIP_TRY(e);
   return kOk;
 }
 int dpf_hip_free(void* ptr) {

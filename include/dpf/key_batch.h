@@ -133,11 +133,16 @@ class DeviceBatchContext {
   size_t next_seeds_cap_ = 0, next_ctrl_cap_ = 0;
   // Expansion cache: the tree leaves of the last call ([key][leaf_stride_]),
   // i.e. the next call's tree nodes (DistributedPointFunction's batched
-  // EvaluateUntil gathers its start seeds from it instead of walking down
+  // EvaluateUntil reads its start seeds from it instead of walking down
   // from the partial evaluations two calls back).  leaf_de_: levels from a
-  // tree index of that call to its leaves.
+  // tree index of that call to its leaves.  Double-buffered: a call reads
+  // leaf_seeds_ and writes leaf_spare_, then the two swap; without room for
+  // the spare, the start seeds are gathered (slots_) and the cache is
+  // rewritten in place.
   void* leaf_seeds_ = nullptr;  // seed | control bit (bit 0)
   size_t leaf_seeds_cap_ = 0;
+  void* leaf_spare_ = nullptr;
+  size_t leaf_spare_cap_ = 0;
   int64_t leaf_stride_ = 0;
   int leaf_level_ = -1;
   int leaf_de_ = 0;

@@ -239,7 +239,9 @@ int dpf_hip_sum_shares_u64(int64_t num_keys, int64_t row_len, int bits, int xor_
  *
  * For key k < num_keys and start node u < num_starts:
  *   start  = (seeds_in[k*in_stride + parent[u]], control_in[...]), or key k's
- *            root (key_seed[k], party[k]) when seeds_in == NULL;
+ *            root (key_seed[k], party[k]) when seeds_in == NULL; with
+ *            control_in == NULL the control bit is bit 0 of the seed (the
+ *            expansion cache layout below) and is cleared before use;
  *   walk   walk_levels levels along path[u] (bit walk_levels-1-j at step j)
  *          with key k's correction words cw_first + j (rows of cw_stride);
  *          after save_after steps (-1 = never) the node is stored at
@@ -278,10 +280,12 @@ int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_lev
  * leaf_cache[k*leaf_stride + (u << expand_levels) + l] (leaf_stride >=
  * num_starts << expand_levels), the node's seed with its control bit in bit 0
  * (clear in every non-root seed).  The next level's tree nodes are among these
- * leaves, so its start seeds are gathered from them (dpf_hip_gather_seeds)
- * instead of re-derived by a path walk from the partial evaluations two calls
- * back (distributed_point_function.cc:351-453).  The
- * leaves must not be the root (depth > 0).  leaf_cache == NULL: no cache. */
+ * leaves, so the next call reads its start seeds straight from them
+ * (seeds_in = the cache, control_in = NULL, parent[u] = the node's cache slot)
+ * instead of re-deriving them by a path walk from the partial evaluations two
+ * calls back (distributed_point_function.cc:351-453).
+ * The leaves must not be the root (depth > 0).  leaf_cache must not overlap
+ * seeds_in (the caller double-buffers).  leaf_cache == NULL: no cache. */
 int dpf_hip_eval_prefix_batch_cached(
     int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
     int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,

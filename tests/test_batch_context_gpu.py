@@ -155,6 +155,16 @@ def test_batch_incremental_without_expansion_cache(levels, plan, sum_mode, monke
     _run(levels, plan, 37, sum_mode, seed=len(levels) + 11)
 
 
+@pytest.mark.parametrize("levels,plan", CASES[:4] + CASES[-3:], ids=lambda x: str(x)[:60])
+@pytest.mark.parametrize("sum_mode", [False, True])
+def test_batch_incremental_cache_in_place(levels, plan, sum_mode, monkeypatch):
+    """DPF_BATCH_CACHE_IN_PLACE=1: the fallback for when no spare cache buffer
+    fits -- the start seeds are gathered out of the cache, which the kernel
+    then rewrites in place.  Same outputs and contexts."""
+    monkeypatch.setenv("DPF_BATCH_CACHE_IN_PLACE", "1")
+    _run(levels, plan, 37, sum_mode, seed=len(levels) + 13)
+
+
 def test_batch_many_prefixes_one_key():
     """Config-5a shape: one key, thousands of prefixes per level."""
     import torch
