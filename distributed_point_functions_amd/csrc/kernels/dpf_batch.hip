@@ -29,9 +29,6 @@
 // registers, then adds them once into exact 192-bit per-element sums.
 // No last-round scheduling fence in this TU (aes_core.h, encryptN): the
 // heavy-hitters kernel measured 0.35% slower with it (24.26 vs 24.18 s per pass).
-#ifndef DPF_BATCH_PAIR_L1
-#define DPF_BATCH_PAIR_L1 0
-#endif
 #ifndef DPF_LAST_ROUND_FENCE
 #define DPF_LAST_ROUND_FENCE 1024
 #endif
@@ -357,26 +354,24 @@ struct GenericV {
 
 // --------------------------------------------------------------------- kernel
 
-// Expands a start node by p.expand_levels levels in registers (children 2i,
-// 2i+1 of node i, distributed_point_function.cc:324-330), then converts every
-// leaf.  The first `dstart` (0 or 1) levels are already expanded: n0 (and n1)
-// with control bits T (bit i for node i).  `sink(l, val)` receives leaf l's
-// value (sum or store).
+// Expands `node` by p.expand_levels levels in registers (children 2i, 2i+1 of
+// node i, distributed_point_function.cc:324-330), then converts every leaf.
+// `sink(l, val)` receives leaf l's value (sum or store).
 template <int MAXE, class V, class Sink>
 __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const BatchLevelParams& p,
-                                                   const V& v, int64_t k, Block4 n0, Block4 n1,
-                                                   uint32_t T, int dstart, int64_t leaf_at,
-                                                   Sink&& sink) {
+                                                   const V& v, int64_t k, Block4 node,
+                                                   uint32_t t, int64_t leaf_at, Sink&& sink) {
   Block4 N[1 << MAXE];
-  N[0] = n0;
-  if constexpr (MAXE > 0) N[1] = n1;
+  uint32_t T = 0;  // bit i = control bit of N[i]
+  N[0] = node;
+  T = t & 1u;
   const int E = p.expand_levels;
   const dpf_block* cws = p.cw_seed + k * p.cw_stride + p.cw_first + p.walk_levels;
   const uint8_t* cl = p.cw_left + k * p.cw_stride + p.cw_first + p.walk_levels;
   const uint8_t* cr = p.cw_right + k * p.cw_stride + p.cw_first + p.walk_levels;
 #pragma unroll
   for (int d = 0; d < MAXE; ++d) {
-    if (d < E && d >= dstart) {
+    if (d < E) {
       const uint4 cs = cw_block(cws + d);
       const uint32_t cc = (uint32_t)(cl[d] & 1) | ((uint32_t)(cr[d] & 1) << 1);
       if (d == 0) {
@@ -407,11 +402,6 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
   }
   // The expansion cache: this start node's 2^E leaves (node and control bit),
   // 2^E consecutive entries per lane.
-#if defined(DPF_PROBE_NO_LEAF_STORE)
-  // Probe build only (tools/): the cache is not written (the next call reads
-  // stale seeds), so a run measures what the stores cost.
-  leaf_at = -1;
-#endif
   if (leaf_at >= 0) {
 #pragma unroll
     for (int i = 0; i < (1 << MAXE); ++i) {
@@ -512,44 +502,18 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
         path_step2k(lk, p.rkl, p.rkd, sa, ta, cw_block(ca + j), cca, sb, tb, cw_block(cb + j), ccb,
                     bit);
       }
-      // 2. the first expansion level of both keys together (ILP4).
-      Block4 ea[2] = {sa, sa}, eb[2] = {sb, sb};
-      uint32_t Ta = ta, Tb = tb;
-      int dstart = 0;
-#if DPF_BATCH_PAIR_L1
-      if (MAXE > 0 && p.expand_levels > 0 && has_b) {
-        const int64_t o = p.cw_first + W;
-        Block4 c[4];
-        uint32_t t4[4];
-        children_step_2k(lk, p.rkl.k, p.rkr.k, sa, ta, cw_block(p.cw_seed + ka * p.cw_stride + o),
-                         (uint32_t)(p.cw_left[ka * p.cw_stride + o] & 1) |
-                             ((uint32_t)(p.cw_right[ka * p.cw_stride + o] & 1) << 1),
-                         sb, tb, cw_block(p.cw_seed + kb * p.cw_stride + o),
-                         (uint32_t)(p.cw_left[kb * p.cw_stride + o] & 1) |
-                             ((uint32_t)(p.cw_right[kb * p.cw_stride + o] & 1) << 1),
-                         c, t4);
-        ea[0] = c[0];
-        ea[1] = c[1];
-        eb[0] = c[2];
-        eb[1] = c[3];
-        Ta = t4[0] | (t4[1] << 1);
-        Tb = t4[2] | (t4[3] << 1);
-        dstart = 1;
-      }
-#endif
-      // 3.-4. the remaining expansion, conversion and sum/store, one key at a time.
+      // 2.-4. expansion, conversion and sum/store, one key at a time.
       for (int which = 0; which < 2; ++which) {
         if (which == 1 && !has_b) break;
         const int64_t k = which ? kb : ka;
         V vk = v;
         vk.key(p, k);
-        const Block4 n0 = which ? eb[0] : ea[0];
-        const Block4 n1 = which ? eb[1] : ea[1];
-        const uint32_t tn = which ? Tb : Ta;
+        const Block4 node = which ? sb : sa;
+        const uint32_t tn = which ? tb : ta;
         const int64_t leaf_at =
             p.leaf_seeds && valid ? k * p.leaf_stride + (u << p.expand_levels) : -1;
         if constexpr (SUM) {
-          expand_and_convert<MAXE>(lk, p, vk, k, n0, n1, tn, dstart, leaf_at,
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_at,
                                    [&](int l, const typename V::Val& val) {
 #pragma unroll
             for (int i = 0; i < (1 << MAXE); ++i)
@@ -557,7 +521,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
           });
         } else {
           char* row = p.out + k * p.out_row + (u << p.expand_levels) * (int64_t)p.epl * p.esz;
-          expand_and_convert<MAXE>(lk, p, vk, k, n0, n1, tn, dstart, leaf_at,
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_at,
                                    [&](int l, const typename V::Val& val) {
             if (valid) vk.store(lk, p, row + (int64_t)l * p.epl * p.esz, val);
           });

@@ -258,28 +258,6 @@ __device__ __forceinline__ void children_step_x2(const LdsLookup& lk, const uint
   }
 }
 
-// children_step for one node each of two keys (own correction words): the four
-// child hashes interleaved (ILP4).  c[0..1], t[0..1]: key a's children.
-__device__ __forceinline__ void children_step_2k(const LdsLookup& lk, const uint32_t* rkl,
-                                                 const uint32_t* rkr, Block4 sa, uint32_t ta,
-                                                 uint4 csa, uint32_t cca, Block4 sb, uint32_t tb,
-                                                 uint4 csb, uint32_t ccb, Block4* c, uint32_t* t) {
-  Block4 h[4] = {sa, sa, sb, sb};
-  const UniformRK rk[4] = {UniformRK{rkl}, UniformRK{rkr}, UniformRK{rkl}, UniformRK{rkr}};
-  dpf_aes::mmo_hashN<4>(h, lk, rk);
-  const uint32_t pt[4] = {ta, ta, tb, tb};
-  const uint4 cs[4] = {csa, csa, csb, csb};
-  const uint32_t cc[4] = {cca, cca, ccb, ccb};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t m = 0u - pt[i];
-    h[i].w0 ^= cs[i].x & m; h[i].w1 ^= cs[i].y & m; h[i].w2 ^= cs[i].z & m; h[i].w3 ^= cs[i].w & m;
-    t[i] = (h[i].w0 & 1u) ^ (pt[i] & ((cc[i] >> (i & 1)) & 1u));
-    h[i].w0 &= ~1u;
-    c[i] = h[i];
-  }
-}
-
 // Path step with a per-lane direction bit (evaluate_prg_hwy.cc:452-486).
 __device__ __forceinline__ void path_step(const LdsLookup& lk, const RoundKeys& rkl,
                                           const RoundKeys& rkd, Block4& s, uint32_t& t,
