@@ -305,8 +305,13 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         // The spare may still be read by work in flight on the stream.
         HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
         if (ctx.leaf_spare_) dpf_hip_free(ctx.leaf_spare_);
+        ctx.leaf_spare_ = nullptr;
         ctx.leaf_spare_cap_ = 0;
-        if (dpf_hip_alloc(&ctx.leaf_spare_, cache_need) == 0) ctx.leaf_spare_cap_ = cache_need;
+        // Only with a quarter of the device left over for everything else.
+        size_t free_b = 0, total_b = 0;
+        if (dpf_hip_mem_info(&free_b, &total_b) == 0 && free_b >= cache_need + total_b / 4 &&
+            dpf_hip_alloc(&ctx.leaf_spare_, cache_need) == 0)
+          ctx.leaf_spare_cap_ = cache_need;
       }
       if (ctx.leaf_spare_ && ctx.leaf_spare_cap_ >= cache_need && !SpareOff()) {
         leaf_seeds = ctx.leaf_spare_;
@@ -317,6 +322,29 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     }
   }
   const bool direct = cached && !gather;  // start seeds read from the cache
+  // The per-call buffers come first: when device memory runs out, the
+  // expansion cache gives way (the spare, then -- unless this call reads it --
+  // the cache itself) and the allocation is retried.
+  bool cache_in_use = cached;  // read by this call's gather or kernel
+  auto ensure = [&](void** p, size_t* cap, size_t bytes) -> Status {
+    Status st = DeviceBatchContext::Ensure(p, cap, bytes);
+    for (int step = 0; !st.ok() && step < 2; ++step) {
+      void** victim = step == 0 ? &ctx.leaf_spare_ : &ctx.leaf_seeds_;
+      size_t* victim_cap = step == 0 ? &ctx.leaf_spare_cap_ : &ctx.leaf_seeds_cap_;
+      if (!*victim || (step == 1 && cache_in_use)) continue;
+      HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+      if (leaf_seeds == *victim) {
+        leaf_seeds = nullptr;  // this call writes no cache
+        swap_cache = false;
+      }
+      dpf_hip_free(*victim);
+      *victim = nullptr;
+      *victim_cap = 0;
+      if (step == 1) ctx.leaf_level_ = -1;
+      st = DeviceBatchContext::Ensure(p, cap, bytes);
+    }
+    return st;
+  };
 
   clk.mark(1);
   // Start-node tables: u = tree index i * 2^s + sub.  Host staging buffers
@@ -358,26 +386,27 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     }
   });
   clk.mark(2);
-  DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.parent_, &ctx.parent_cap_, U * sizeof(int32_t)));
-  DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.path_, &ctx.path_cap_, U * sizeof(dpf_block)));
-  DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.save_, &ctx.save_cap_, U * sizeof(int32_t)));
+  DPF_RETURN_IF_ERROR(ensure(&ctx.parent_, &ctx.parent_cap_, U * sizeof(int32_t)));
+  DPF_RETURN_IF_ERROR(ensure(&ctx.path_, &ctx.path_cap_, U * sizeof(dpf_block)));
+  DPF_RETURN_IF_ERROR(ensure(&ctx.save_, &ctx.save_cap_, U * sizeof(int32_t)));
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.parent_, parent.data(), U * sizeof(int32_t), stream));
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.path_, path.data(), U * sizeof(dpf_block), stream));
   HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.save_, save.data(), U * sizeof(int32_t), stream));
   if (update_ctx || gather) {
-    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.next_seeds_, &ctx.next_seeds_cap_,
+    DPF_RETURN_IF_ERROR(ensure(&ctx.next_seeds_, &ctx.next_seeds_cap_,
                                                    K * T * sizeof(dpf_block)));
-    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.next_ctrl_, &ctx.next_ctrl_cap_, K * T));
+    DPF_RETURN_IF_ERROR(ensure(&ctx.next_ctrl_, &ctx.next_ctrl_cap_, K * T));
   }
   if (gather) {
     // The start seeds (and, with update_ctx, the new partial evaluations),
     // read before the kernel rewrites the cache.
-    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.slots_, &ctx.slots_cap_, T * sizeof(int64_t)));
+    DPF_RETURN_IF_ERROR(ensure(&ctx.slots_, &ctx.slots_cap_, T * sizeof(int64_t)));
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.slots_, slots.data(), T * sizeof(int64_t), stream));
     HIP_RETURN_IF_ERROR(dpf_hip_gather_seeds(
         K, T, static_cast<const int64_t*>(ctx.slots_), static_cast<const dpf_block*>(ctx.leaf_seeds_),
         ctx.leaf_stride_, static_cast<dpf_block*>(ctx.next_seeds_),
         static_cast<uint8_t*>(ctx.next_ctrl_), stream));
+    cache_in_use = false;  // copied out; from here on only the write target
     const size_t cache_need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
     if (ctx.leaf_seeds_cap_ < cache_need) {
       // Regrow once the gather has read the old cache.
@@ -394,7 +423,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     for (int64_t i = 0; i < P; ++i)
       offsets[i] = prefix_map[i].first * block + prefix_map[i].second * cnt;
     DPF_RETURN_IF_ERROR(
-        DeviceBatchContext::Ensure(&ctx.offsets_, &ctx.offsets_cap_, P * sizeof(int64_t)));
+        ensure(&ctx.offsets_, &ctx.offsets_cap_, P * sizeof(int64_t)));
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.offsets_, offsets.data(), P * sizeof(int64_t), stream));
   }
 
@@ -424,10 +453,10 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   if (native_sum) {
     void* target = device_out;
     if (!identity) {
-      DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage_, &ctx.stage_cap_, n_blk * esz));
+      DPF_RETURN_IF_ERROR(ensure(&ctx.stage_, &ctx.stage_cap_, n_blk * esz));
       target = ctx.stage_;
     }
-    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(
+    DPF_RETURN_IF_ERROR(ensure(
         &ctx.workspace_, &ctx.workspace_cap_, n_blk * f.leaves.size() * 3 * sizeof(uint64_t)));
     DPF_RETURN_IF_ERROR(launch(1, target, static_cast<uint64_t*>(ctx.workspace_)));
     if (!identity)
@@ -436,11 +465,11 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   } else if (sum) {
     // Value types without an on-device key sum in the kernel: per-key rows,
     // then a group sum over the rows.
-    DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage_, &ctx.stage_cap_, K * n_blk * esz));
+    DPF_RETURN_IF_ERROR(ensure(&ctx.stage_, &ctx.stage_cap_, K * n_blk * esz));
     DPF_RETURN_IF_ERROR(launch(0, ctx.stage_, nullptr));
     void* target = device_out;
     if (!identity) {
-      DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage2_, &ctx.stage2_cap_, n_blk * esz));
+      DPF_RETURN_IF_ERROR(ensure(&ctx.stage2_, &ctx.stage2_cap_, n_blk * esz));
       target = ctx.stage2_;
     }
     HIP_RETURN_IF_ERROR(dpf_hip_sum_rows(K, n_blk, &desc, ctx.stage_, target, stream));
@@ -450,7 +479,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   } else {
     void* target = device_out;
     if (!identity) {
-      DPF_RETURN_IF_ERROR(DeviceBatchContext::Ensure(&ctx.stage_, &ctx.stage_cap_, K * n_blk * esz));
+      DPF_RETURN_IF_ERROR(ensure(&ctx.stage_, &ctx.stage_cap_, K * n_blk * esz));
       target = ctx.stage_;
     }
     DPF_RETURN_IF_ERROR(launch(0, target, nullptr));

@@ -898,6 +898,11 @@ int dpf_hip_alloc(void** ptr, size_t bytes) {
   HIP_TRY(e);
   return kOk;
 }
+int dpf_hip_mem_info(size_t* free_bytes, size_t* total_bytes) {
+  if (!free_bytes || !total_bytes) return fail(kInvalidArgument, "NULL pointer");
+  HIP_TRY(hipMemGetInfo(free_bytes, total_bytes));
+  return kOk;
+}
 int dpf_hip_free(void* ptr) {
   if (ptr) HIP_TRY(hipFree(ptr));
   return kOk;

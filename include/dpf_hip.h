@@ -82,6 +82,8 @@ int dpf_hip_device_count(int* count);
 int dpf_hip_set_device(int device);
 int dpf_hip_alloc(void** ptr, size_t bytes);
 int dpf_hip_free(void* ptr);
+/* Free and total device memory of the current device (hipMemGetInfo). */
+int dpf_hip_mem_info(size_t* free_bytes, size_t* total_bytes);
 int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 /* Page-locked host memory, and an H2D copy that does not wait: `src` must be
  * page-locked (dpf_hip_host_alloc) and stay unchanged until `stream` has run
