@@ -72,6 +72,7 @@ bool SpareOff() {
 struct PhaseClock {
   std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
   void mark(int phase) {
+    if (!g_timing_on) return;
     auto now = std::chrono::steady_clock::now();
     g_timing.t[phase] += std::chrono::duration<double>(now - last).count();
     last = now;
@@ -79,15 +80,79 @@ struct PhaseClock {
 };
 }  // namespace
 
-Status DeviceBatchContext::Ensure(void** p, size_t* cap, size_t bytes) {
-  if (*p && *cap >= bytes) return OkStatus();
-  if (*p) dpf_hip_free(*p);
+// DPF_BATCH_ALLOC_LIMIT=<bytes>: a test hook that makes a batch context behave
+// as if the device had only that much memory for it -- an allocation that
+// would take the context's total above the limit fails like hipMalloc's
+// out-of-memory, and MemInfo reports the limit -- so the expansion cache's
+// fallbacks (no spare, eviction and retry, RESOURCE_EXHAUSTED) run
+// deterministically.  Read per call.
+size_t AllocLimit() {
+  const char* v = std::getenv("DPF_BATCH_ALLOC_LIMIT");
+  return v && *v ? static_cast<size_t>(std::strtoull(v, nullptr, 10)) : 0;
+}
+
+bool DeviceBatchContext::TryAlloc(void** p, size_t* cap, size_t bytes) {
   *p = nullptr;
   *cap = 0;
-  const size_t want = std::max<size_t>(bytes, 256);
-  HIP_RETURN_IF_ERROR(dpf_hip_alloc(p, want));
-  *cap = want;
+  const size_t limit = AllocLimit();
+  if (limit && device_bytes_ + bytes > limit) return false;
+  if (dpf_hip_alloc(p, bytes) != 0) {
+    *p = nullptr;
+    return false;
+  }
+  *cap = bytes;
+  device_bytes_ += bytes;
+  return true;
+}
+
+void DeviceBatchContext::Release(void** p, size_t* cap) {
+  if (*p) dpf_hip_free(*p);
+  device_bytes_ -= std::min(device_bytes_, *cap);
+  *p = nullptr;
+  *cap = 0;
+}
+
+void DeviceBatchContext::MemInfo(size_t* free_bytes, size_t* total_bytes) const {
+  *free_bytes = *total_bytes = 0;
+  if (const size_t limit = AllocLimit()) {
+    *total_bytes = limit;
+    *free_bytes = limit - std::min(limit, device_bytes_);
+    return;
+  }
+  (void)dpf_hip_mem_info(free_bytes, total_bytes);
+}
+
+Status DeviceBatchContext::Ensure(void** p, size_t* cap, size_t bytes) {
+  if (fail_next_ > 0 && fail_skip_ > 0) {
+    --fail_skip_;
+  } else if (fail_next_ > 0) {
+    --fail_next_;
+    Release(p, cap);
+    ++events_.alloc_failures;
+    return ResourceExhaustedError("Memory allocation error");
+  }
+  if (*p && *cap >= bytes) return OkStatus();
+  Release(p, cap);
+  if (!TryAlloc(p, cap, std::max<size_t>(bytes, 256))) {
+    ++events_.alloc_failures;
+    return ResourceExhaustedError("Memory allocation error");  // cc:289-291
+  }
   return OkStatus();
+}
+
+void DeviceBatchContext::ReleaseExpansionCache() {
+  Release(&leaf_seeds_, &leaf_seeds_cap_);
+  Release(&leaf_spare_, &leaf_spare_cap_);
+  Release(&slots_, &slots_cap_);
+  leaf_level_ = -1;
+}
+
+void DeviceBatchContext::Reset() {
+  previous_hierarchy_level_ = -1;
+  partial_evaluations_level_ = -1;
+  partial_prefixes_.clear();
+  (void)dpf_hip_stream_sync(nullptr);  // work still reading the cache
+  ReleaseExpansionCache();
 }
 
 DeviceBatchContext::~DeviceBatchContext() {
@@ -163,7 +228,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
 
   PhaseClock clk;
-  ++g_timing.calls;
+  if (g_timing_on) ++g_timing.calls;
   // Unique tree indices in first-seen order and each prefix's (tree index,
   // block index) (h:718-742).
   const int64_t P = static_cast<int64_t>(prefixes.size());
@@ -287,15 +352,23 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   void* leaf_seeds = nullptr;
   bool swap_cache = false;
   bool gather = false;
+  // Headroom left on the device for everything else (the caller's buffers,
+  // a second context): a quarter of it for the spare, an eighth for the cache.
+  auto fits = [&](size_t bytes, size_t reserve_div) {
+    size_t free_b = 0, total_b = 0;
+    ctx.MemInfo(&free_b, &total_b);
+    return free_b >= bytes + total_b / reserve_div;
+  };
   if (g_cache_on && hierarchy_level < H - 1 && Dh > 0) {
     const size_t cache_need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
     if (!cached) {
       // The current cache is not read by this call: rewrite (or regrow) it.
+      ctx.leaf_level_ = -1;  // until this call has written it
       if (ctx.leaf_seeds_cap_ < cache_need) {
         HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
-        if (ctx.leaf_seeds_) dpf_hip_free(ctx.leaf_seeds_);
-        ctx.leaf_seeds_cap_ = 0;
-        if (dpf_hip_alloc(&ctx.leaf_seeds_, cache_need) == 0) ctx.leaf_seeds_cap_ = cache_need;
+        ctx.Release(&ctx.leaf_seeds_, &ctx.leaf_seeds_cap_);
+        if (!fits(cache_need, 8) || !ctx.TryAlloc(&ctx.leaf_seeds_, &ctx.leaf_seeds_cap_, cache_need))
+          ++ctx.events_.cache_refused;
       }
       leaf_seeds = ctx.leaf_seeds_;
     } else {
@@ -304,20 +377,16 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
       } else if (ctx.leaf_spare_cap_ < cache_need) {
         // The spare may still be read by work in flight on the stream.
         HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
-        if (ctx.leaf_spare_) dpf_hip_free(ctx.leaf_spare_);
-        ctx.leaf_spare_ = nullptr;
-        ctx.leaf_spare_cap_ = 0;
-        // Only with a quarter of the device left over for everything else.
-        size_t free_b = 0, total_b = 0;
-        if (dpf_hip_mem_info(&free_b, &total_b) == 0 && free_b >= cache_need + total_b / 4 &&
-            dpf_hip_alloc(&ctx.leaf_spare_, cache_need) == 0)
-          ctx.leaf_spare_cap_ = cache_need;
+        ctx.Release(&ctx.leaf_spare_, &ctx.leaf_spare_cap_);
+        if (!fits(cache_need, 4) || !ctx.TryAlloc(&ctx.leaf_spare_, &ctx.leaf_spare_cap_, cache_need))
+          ++ctx.events_.spare_refused;
       }
       if (ctx.leaf_spare_ && ctx.leaf_spare_cap_ >= cache_need && !SpareOff()) {
         leaf_seeds = ctx.leaf_spare_;
         swap_cache = true;
       } else {
         gather = true;  // leaf_seeds is set once the gather is enqueued
+        ++ctx.events_.in_place;
       }
     }
   }
@@ -327,7 +396,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   // the cache itself) and the allocation is retried.
   bool cache_in_use = cached;  // read by this call's gather or kernel
   auto ensure = [&](void** p, size_t* cap, size_t bytes) -> Status {
-    Status st = DeviceBatchContext::Ensure(p, cap, bytes);
+    Status st = ctx.Ensure(p, cap, bytes);
     for (int step = 0; !st.ok() && step < 2; ++step) {
       void** victim = step == 0 ? &ctx.leaf_spare_ : &ctx.leaf_seeds_;
       size_t* victim_cap = step == 0 ? &ctx.leaf_spare_cap_ : &ctx.leaf_seeds_cap_;
@@ -337,11 +406,10 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         leaf_seeds = nullptr;  // this call writes no cache
         swap_cache = false;
       }
-      dpf_hip_free(*victim);
-      *victim = nullptr;
-      *victim_cap = 0;
+      ctx.Release(victim, victim_cap);
+      ++(step == 0 ? ctx.events_.evicted_spare : ctx.events_.evicted_cache);
       if (step == 1) ctx.leaf_level_ = -1;
-      st = DeviceBatchContext::Ensure(p, cap, bytes);
+      st = ctx.Ensure(p, cap, bytes);
     }
     return st;
   };
@@ -407,13 +475,14 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         ctx.leaf_stride_, static_cast<dpf_block*>(ctx.next_seeds_),
         static_cast<uint8_t*>(ctx.next_ctrl_), stream));
     cache_in_use = false;  // copied out; from here on only the write target
+    ctx.leaf_level_ = -1;  // rewritten in place by this call's kernel
     const size_t cache_need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
     if (ctx.leaf_seeds_cap_ < cache_need) {
       // Regrow once the gather has read the old cache.
       HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
-      dpf_hip_free(ctx.leaf_seeds_);
-      ctx.leaf_seeds_cap_ = 0;
-      if (dpf_hip_alloc(&ctx.leaf_seeds_, cache_need) == 0) ctx.leaf_seeds_cap_ = cache_need;
+      ctx.Release(&ctx.leaf_seeds_, &ctx.leaf_seeds_cap_);
+      if (!fits(cache_need, 8) || !ctx.TryAlloc(&ctx.leaf_seeds_, &ctx.leaf_seeds_cap_, cache_need))
+        ++ctx.events_.cache_refused;
     }
     leaf_seeds = ctx.leaf_seeds_;
   }
@@ -496,6 +565,12 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   ctx.leaf_level_ = leaf_seeds ? hierarchy_level : -1;
   ctx.leaf_de_ = dE;
   ctx.leaf_stride_ = leaf_stride;
+  if (hierarchy_level == H - 1 && (ctx.leaf_seeds_ || ctx.leaf_spare_)) {
+    // Nothing reads the cache after the last level: give its memory back
+    // once this call's kernel has read it.
+    HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+    ctx.ReleaseExpansionCache();
+  }
   if (g_timing_on) dpf_hip_stream_sync(stream);  // attribute device time to its phase
   clk.mark(4);
   // Context update (cc:435-451, 494-496).

@@ -482,13 +482,20 @@ struct UntilTiming {
   }
 };
 UntilTiming g_until_timing;
+std::mutex g_until_timing_mu;  // the counters are process-wide; calls on several objects race
 const bool g_until_timing_on = std::getenv("DPF_HOST_TIMING") != nullptr;
 struct UntilClock {
   std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+  void count_call() {
+    if (!g_until_timing_on) return;
+    std::lock_guard<std::mutex> lock(g_until_timing_mu);
+    ++g_until_timing.calls;
+  }
   void mark(int phase) {
     if (!g_until_timing_on) return;
     auto now = std::chrono::steady_clock::now();
     // The first 100 calls (allocations, page-locked buffers) are not counted.
+    std::lock_guard<std::mutex> lock(g_until_timing_mu);
     if (g_until_timing.calls > 100)
       g_until_timing.t[phase] += std::chrono::duration<double>(now - last).count();
     last = now;
@@ -565,7 +572,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   // value correction of this level (h:761-780) is parsed before device work.
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
-  if (g_until_timing_on) ++g_until_timing.calls;
+  clk.count_call();
   clk.mark(0);
   std::vector<uint128> vcw;
   auto parse_vcw = [&]() -> Status {

@@ -457,6 +457,21 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def_property_readonly("partial_evaluations_level", &PyBatchContext::PartialEvaluationsLevel)
       .def_property_readonly("expansion_cache_level", &PyBatchContext::ExpansionCacheLevel)
       .def_property_readonly("num_partial_evaluations", &PyBatchContext::NumPartialEvaluations)
+      .def_property_readonly("device_bytes", [](const PyBatchContext& c) { return c.ctx->device_bytes(); })
+      .def_property_readonly("cache_events", [](const PyBatchContext& c) {
+        const auto& e = c.ctx->cache_events();
+        py::dict d;
+        d["cache_refused"] = e.cache_refused;
+        d["spare_refused"] = e.spare_refused;
+        d["in_place"] = e.in_place;
+        d["evicted_spare"] = e.evicted_spare;
+        d["evicted_cache"] = e.evicted_cache;
+        d["alloc_failures"] = e.alloc_failures;
+        return d;
+      })
+      .def("fail_next_allocations_for_testing",
+           [](PyBatchContext& c, int n, int skip) { c.ctx->FailNextAllocationsForTesting(n, skip); },
+           py::arg("n"), py::arg("skip") = 0)
       .def("reset", [](PyBatchContext& c) { c.ctx->Reset(); });
   py::class_<PyKeyBatch>(m, "KeyBatch")
       .def_property_readonly("num_keys", &PyKeyBatch::NumKeys)

@@ -5,6 +5,7 @@
 #define DPF_HOST_HOST_UTIL_H_
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -40,6 +41,13 @@ inline Status FromHip(int code) {
 // (dpf_hip_memcpy_d2h_staged).  Returns a dpf_hip status code.
 inline int CopyToHostSink(const HostSink& sink, void* dst, const void* src, size_t bytes,
                           void* stream) {
+  if (sink.chunk && (!dst || bytes < DPF_HIP_REGISTER_MIN_BYTES)) {
+    auto consume = [](void* ctx, const void* chunk, size_t offset, size_t len) {
+      (*static_cast<const HostSink*>(ctx)).chunk(static_cast<const uint8_t*>(chunk), offset, len);
+    };
+    return dpf_hip_memcpy_d2h_chunked(src, bytes, sink.align, consume,
+                                      const_cast<HostSink*>(&sink), stream);
+  }
   if (!sink.grow) return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
   auto before = [](void* ctx, size_t ready) {
     (*static_cast<const std::function<void(size_t)>*>(ctx))(ready);
@@ -92,13 +100,25 @@ struct U128Hash {
   }
 };
 
-// fn(lo, hi) over [0, n) split across host threads (at most 16) when n is
-// large enough to pay for them; inline otherwise.
+// Host threads the library's parallel loops may use: DPF_HOST_THREADS when
+// set (>= 1), else min(16, hardware threads) -- 16 is the GPU box's CPU share
+// per GPU.
+inline int HostThreads() {
+  static const int n = [] {
+    const char* e = std::getenv("DPF_HOST_THREADS");
+    const int v = e ? std::atoi(e) : 0;
+    if (v >= 1) return v;
+    return static_cast<int>(std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())));
+  }();
+  return n;
+}
+
+// fn(lo, hi) over [0, n) split across host threads (at most HostThreads())
+// when n is large enough to pay for them; inline otherwise.
 template <typename F>
 void ParallelFor(int64_t n, F fn, int64_t min_per_thread = int64_t{1} << 15) {
   int threads = static_cast<int>(std::min<int64_t>(
-      std::min<int64_t>(16, std::max(1u, std::thread::hardware_concurrency())),
-      n / std::max<int64_t>(min_per_thread, 1)));
+      HostThreads(), n / std::max<int64_t>(min_per_thread, 1)));
   if (threads <= 1) {
     if (n > 0) fn(int64_t{0}, n);
     return;
@@ -112,9 +132,8 @@ void ParallelFor(int64_t n, F fn, int64_t min_per_thread = int64_t{1} << 15) {
 
 // Number of chunks ParallelChunks uses for n items.
 inline int NumChunks(int64_t n, int64_t min_per_chunk = int64_t{1} << 15) {
-  const int64_t hw = std::max(1u, std::thread::hardware_concurrency());
   return static_cast<int>(std::max<int64_t>(
-      1, std::min<int64_t>(std::min<int64_t>(16, hw), n / std::max<int64_t>(min_per_chunk, 1))));
+      1, std::min<int64_t>(HostThreads(), n / std::max<int64_t>(min_per_chunk, 1))));
 }
 
 // fn(chunk, lo, hi) for `chunks` contiguous chunks of [0, n), one thread each.

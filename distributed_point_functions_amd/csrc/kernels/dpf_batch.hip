@@ -44,6 +44,10 @@ using namespace dpf_rt;
 
 namespace {
 
+// Which kernel the calling thread's last dpf_hip_eval_prefix_batch_cached ran
+// (dpf_hip_last_batch_kernel: dispatch checks in the tests).
+thread_local const char* g_last_batch_kernel = "";
+
 struct BatchLevelParams {
   int64_t num_keys;
   int64_t num_starts;       // U
@@ -774,7 +778,47 @@ int dpf_hip_eval_prefix_batch_cached(
     p.rkv = expand_key(key_value);
     p.rkd = xor_keys(p.rkl, p.rkr);
     int b = 0;
-    if (fast_int(desc)) {
+    // The steady state of heavy hitters (start seeds from the expansion cache
+    // or a gather, no walk, two expanded levels, IntModN<uint32_t> sums): the
+    // lean kernel of dpf_batch_hh.hip.  DPF_BATCH_NO_LEAN=1 keeps the general
+    // kernel (A/B and test hook).
+    const char* no_lean_env = getenv("DPF_BATCH_NO_LEAN");
+    const bool no_lean = no_lean_env && no_lean_env[0] == '1';
+    if (sum && !no_lean && walk_levels == 0 && expand_levels == 2 && seeds_in &&
+        elements_per_leaf == 1 && mod32_eligible(desc, &b) && nl <= 2 && (nl == 1 || b == 2)) {
+      HHLevelArgs a;
+      memset(&a, 0, sizeof(a));
+      a.num_keys = num_keys;
+      a.num_starts = num_starts;
+      a.cw_level = cw_first;
+      a.cw_stride = cw_stride;
+      a.seeds_in = seeds_in;
+      a.ctrl_in = control_in;
+      a.in_stride = in_stride;
+      a.parent = parent;
+      a.save_index = (save_after == 0 && seeds_out) ? save_index : nullptr;
+      a.seeds_out = seeds_out;
+      a.ctrl_out = control_out;
+      a.out_stride = out_stride;
+      a.cw_seed = cw_seed;
+      a.cw_left = cw_left;
+      a.cw_right = cw_right;
+      a.vcw = value_correction;
+      a.vcw_stride = p.vcw_stride;
+      a.party = party;
+      a.wide = p.wide;
+      a.leaf_seeds = p.leaf_seeds;
+      a.leaf_stride = p.leaf_stride;
+      a.nl = nl;
+      a.b = b;
+      for (int k = 0; k < nl; ++k) a.mod[k] = (uint32_t)desc->mod_low[k];
+      a.key_left = key_left;
+      a.key_right = key_right;
+      a.key_value = key_value;
+      st = launch_hh_level(a, s);
+      g_last_batch_kernel = "hh_level";
+    } else if (fast_int(desc)) {
+      g_last_batch_kernel = "batch_level/fast";
       const int xm = desc->kind[0] == DPF_LEAF_XOR;
       st = sum ? launch_batch_fast<true>(p, desc->bits[0], xm, s)
                : launch_batch_fast<false>(p, desc->bits[0], xm, s);
@@ -783,7 +827,9 @@ int dpf_hip_eval_prefix_batch_cached(
       // two ILP2 pairs on heavy hitters); tuples of <= 2 leaves use 2-wide
       // accumulators (117 instead of 128 VGPRs).
       st = nl <= 2 ? launch_mod32<2, true>(p, desc, b, sum, s) : launch_mod32<4, true>(p, desc, b, sum, s);
+      g_last_batch_kernel = "batch_level/mod32";
     } else {
+      g_last_batch_kernel = "batch_level/generic";
       GenericV v;
       memset(&v, 0, sizeof(v));
       v.g.d = *desc;
@@ -802,6 +848,8 @@ int dpf_hip_eval_prefix_batch_cached(
   }
   return kOk;
 }
+
+const char* dpf_hip_last_batch_kernel(void) { return g_last_batch_kernel; }
 
 int dpf_hip_sum_rows(int64_t num_rows, int64_t row_len, const dpf_value_desc* desc,
                      const void* in, void* out, void* stream) {

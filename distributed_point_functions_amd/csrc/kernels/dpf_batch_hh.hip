@@ -1,0 +1,278 @@
+// dpf_batch_hh.hip -- the heavy-hitters level of a key batch (SURVEY.md config
+// 5b) in its steady state: every key's start seeds come from the previous
+// call's expansion cache (no path walk), each start node is expanded two tree
+// levels, its four leaves are hashed, sampled as Tuple<IntModN<uint32_t, N>...>
+// / IntModN<uint32_t, N> values, corrected, and summed over the keys.  This is
+// what batch_level_kernel<Mod32V, 2, true> (dpf_batch.hip) computes for
+// walk_levels == 0 and expand_levels == 2 -- ExpandSeeds (distributed_point_
+// function.cc:271-349) + HashExpandedSeeds (cc:500-524) + the correction loop
+// (h:785-808) + the sampling of value_type_helpers.h:286-311, 415-443 -- in a
+// kernel stripped to that shape: one key at a time (no second key's node held
+// across the first's work), no path state, a small argument block, so the AES
+// chains keep many more LDS lookups in flight at 4 waves per SIMD (r13: the
+// general kernel's schedule waited on LDS every ~2 lookups, VGPR-bound).
+// Built with the iterative-ilp scheduler (build_native.py).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../../include/dpf_hip.h"
+#include "dpf_device.h"
+#include "dpf_runtime.h"
+
+using namespace dpf_rt;
+
+// Waves per SIMD: 4 = 1024-thread workgroups at <= 128 VGPRs (the other
+// kernels' shape); 3 = 768 threads at <= 168 VGPRs (more lookups in flight
+// per wave, fewer waves).
+#ifndef DPF_HH_WAVES
+#define DPF_HH_WAVES 4
+#endif
+// 1: the MMO feed-forward sigma(x) is recomputed from the leaf seed after the
+// encryption instead of being held through it (8 fewer live VGPRs per leaf pair).
+#ifndef DPF_HH_RESIGMA
+#define DPF_HH_RESIGMA 1
+#endif
+
+namespace {
+
+constexpr int kHHBlock = 256 * DPF_HH_WAVES;
+
+struct HHParams {
+  int64_t num_keys;
+  int64_t num_starts;
+  int64_t chunk_keys;
+  int64_t waves_per_chunk;
+  int64_t num_threads;
+  int cw_level;    // correction word of the first expanded level
+  int cw_stride;   // correction words per key row
+  int save;        // 1: store each start node as the key's new partial evaluation
+  int nl;          // tuple leaves (1 or 2)
+  int b;           // value blocks hashed per leaf (1 or 2)
+  const dpf_block* seeds_in;  // [k][in_stride]
+  const uint8_t* ctrl_in;     // NULL: control bit in bit 0 of the seed (expansion cache)
+  int64_t in_stride;
+  const int32_t* parent;
+  const int32_t* save_index;
+  dpf_block* seeds_out;
+  uint8_t* ctrl_out;
+  int64_t out_stride;
+  const dpf_block* cw_seed;
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  const dpf_block* vcw;
+  int vcw_stride;
+  const uint8_t* party;
+  unsigned long long* wide;  // [start << 2 | leaf][nl][3]
+  dpf_block* leaf_seeds;     // NULL: no expansion cache written
+  int64_t leaf_stride;
+  Div32 div[2];
+  RoundKeys rkl, rkr, rkv;
+};
+
+// value = sampled IntModN elements of one leaf (value_type_helpers.h:286-311):
+// r0 = block mod N0; r1 = ((block / N0) << 32 | next 4 bytes) mod N1.
+__device__ __forceinline__ void sample2(const HHParams& p, const Block4& h0, uint32_t w4,
+                                        uint32_t out[2]) {
+  const uint32_t blk[4] = {h0.w0, h0.w1, h0.w2, h0.w3};
+  uint32_t q[3];
+  out[0] = divmod128(blk, p.div[0], q);
+  if (p.nl > 1) {
+    const uint32_t nb[4] = {w4, q[0], q[1], q[2]};
+    uint32_t q2[3];
+    out[1] = divmod128(nb, p.div[1], q2);
+  } else {
+    out[1] = 0;
+  }
+}
+
+__device__ __forceinline__ uint32_t mod_add(uint32_t a, uint32_t b, uint32_t n) {
+  const uint32_t s = a + b;
+  return (s < a || s >= n) ? s - n : s;
+}
+
+// MMO hashes of two leaves' blocks x0, x0 + 1, x1, x1 + 1 (cc:500-524), ILP4.
+__device__ __forceinline__ void hash_leaf_pair(const LdsLookup& lk, const uint32_t* rkv, Block4 x0,
+                                               Block4 x1, Block4 h[4]) {
+  const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
+#if DPF_HH_RESIGMA
+  h[0] = dpf_aes::sigma(x0);
+  h[1] = dpf_aes::sigma(add_small(x0, 1u));
+  h[2] = dpf_aes::sigma(x1);
+  h[3] = dpf_aes::sigma(add_small(x1, 1u));
+  dpf_aes::encryptN<4>(h, lk, rk);
+  const Block4 s[4] = {dpf_aes::sigma(x0), dpf_aes::sigma(add_small(x0, 1u)), dpf_aes::sigma(x1),
+                       dpf_aes::sigma(add_small(x1, 1u))};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    h[i] = Block4{h[i].w0 ^ s[i].w0, h[i].w1 ^ s[i].w1, h[i].w2 ^ s[i].w2, h[i].w3 ^ s[i].w3};
+#else
+  h[0] = x0;
+  h[1] = add_small(x0, 1u);
+  h[2] = x1;
+  h[3] = add_small(x1, 1u);
+  dpf_aes::mmo_hashN<4>(h, lk, rk);
+#endif
+}
+
+__global__ __launch_bounds__(kHHBlock) __attribute__((amdgpu_waves_per_eu(DPF_HH_WAVES, DPF_HH_WAVES)))
+void hh_level_kernel(HHParams p) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const int64_t U = p.num_starts;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.num_threads;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t wave = g >> 6;
+    const int64_t chunk = (int64_t)__builtin_amdgcn_readfirstlane((int)(wave / p.waves_per_chunk));
+    const int64_t u_raw = (wave - chunk * p.waves_per_chunk) * 64 + (g & 63);
+    const bool valid = u_raw < U;
+    const int64_t u = valid ? u_raw : U - 1;
+    const int64_t k_begin = chunk * p.chunk_keys;
+    const int64_t k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
+    const int32_t par = p.parent[u];
+    const int32_t save = p.save && valid ? p.save_index[u] : -1;
+    uint32_t acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = 0;
+    for (int64_t k = k_begin; k < k_end; ++k) {
+      Block4 s = load_block(p.seeds_in + k * p.in_stride + par);
+      uint32_t t;
+      if (p.ctrl_in) {
+        t = p.ctrl_in[k * p.in_stride + par] & 1u;
+      } else {
+        t = s.w0 & 1u;
+        s.w0 &= ~1u;
+      }
+      if (save >= 0) {
+        store_block(p.seeds_out + k * p.out_stride + save, s);
+        p.ctrl_out[k * p.out_stride + save] = (uint8_t)t;
+      }
+      // Two tree levels (cc:304-347): the node's children (ILP2), then both
+      // children's children (ILP4); leaf order 0..3 = LL, LR, RL, RR.
+      const int64_t cwi = k * p.cw_stride + p.cw_level;
+      const uint4 cs0 = make_uint4((uint32_t)p.cw_seed[cwi].low, (uint32_t)(p.cw_seed[cwi].low >> 32),
+                                   (uint32_t)p.cw_seed[cwi].high, (uint32_t)(p.cw_seed[cwi].high >> 32));
+      const uint32_t cc0 = (uint32_t)(p.cw_left[cwi] & 1) | ((uint32_t)(p.cw_right[cwi] & 1) << 1);
+      Block4 c0, c1;
+      uint32_t t0, t1;
+      children_step(lk, p.rkl.k, p.rkr.k, s, t, cs0, cc0, c0, t0, c1, t1);
+      const uint4 cs1 = make_uint4(
+          (uint32_t)p.cw_seed[cwi + 1].low, (uint32_t)(p.cw_seed[cwi + 1].low >> 32),
+          (uint32_t)p.cw_seed[cwi + 1].high, (uint32_t)(p.cw_seed[cwi + 1].high >> 32));
+      const uint32_t cc1 =
+          (uint32_t)(p.cw_left[cwi + 1] & 1) | ((uint32_t)(p.cw_right[cwi + 1] & 1) << 1);
+      Block4 L[4];
+      uint32_t tl[4];
+      children_step_x2(lk, p.rkl.k, p.rkr.k, c0, t0, c1, t1, cs1, cc1, L, tl);
+      if (p.leaf_seeds && valid) {
+        dpf_block* o = p.leaf_seeds + k * p.leaf_stride + (u << 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          Block4 c = L[i];
+          c.w0 |= tl[i];
+          store_block(o + i, c);
+        }
+      }
+      // Value hashes (cc:500-524): two leaves' b blocks per ILP4 group.
+      const int party = p.party[k] & 1;
+      const dpf_block* vc = p.vcw + k * p.vcw_stride;
+      const uint32_t corr[2] = {(uint32_t)vc[0].low, p.nl > 1 ? (uint32_t)vc[1].low : 0u};
+      const UniformRK rk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
+                               UniformRK{p.rkv.k}};
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        Block4 h[4];
+        if (p.b == 2) {
+          hash_leaf_pair(lk, p.rkv.k, L[2 * pr], L[2 * pr + 1], h);
+        } else {
+          h[0] = L[2 * pr];
+          h[2] = L[2 * pr + 1];
+          Block4 two[2] = {h[0], h[2]};
+          dpf_aes::mmo_hashN<2>(two, lk, rk);
+          h[0] = two[0];
+          h[2] = two[1];
+          h[1] = h[3] = Block4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int leaf = 2 * pr + j;
+          uint32_t v[2];
+          sample2(p, h[2 * j], h[2 * j + 1].w0, v);
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            if (e < p.nl) {
+              const uint32_t n = p.div[e].n;
+              uint32_t r = v[e];
+              if (tl[leaf]) r = mod_add(r, corr[e], n);          // int_mod_n.h:116-120
+              if (party == 1) r = r == 0 ? 0u : n - r;            // int_mod_n.h:208-218
+              acc[leaf][e] = mod_add(acc[leaf][e], r, n);
+            }
+          }
+        }
+      }
+    }
+    if (valid && k_begin < k_end) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (e < p.nl && acc[i][e]) wide_add(p.wide + (((u << 2) + i) * p.nl + e) * 3, (u128)acc[i][e]);
+    }
+  }
+}
+
+}  // namespace
+
+namespace dpf_rt {
+
+int launch_hh_level(const HHLevelArgs& a, hipStream_t s) {
+  if (a.nl < 1 || a.nl > 2 || (a.b != 1 && a.b != 2) || (a.nl == 2 && a.b != 2))
+    return fail(kUnimplemented, "hh_level_kernel: unsupported value type");
+  HHParams p;
+  memset(&p, 0, sizeof(p));
+  p.num_keys = a.num_keys;
+  p.num_starts = a.num_starts;
+  p.waves_per_chunk = (a.num_starts + 63) / 64;
+  const int64_t want_waves = (int64_t)num_cus() * (kBlock / 64) * 4;
+  int64_t chunks = (want_waves + p.waves_per_chunk - 1) / p.waves_per_chunk;
+  if (chunks > a.num_keys) chunks = a.num_keys;
+  if (chunks < 1) chunks = 1;
+  p.chunk_keys = (a.num_keys + chunks - 1) / chunks;
+  chunks = (a.num_keys + p.chunk_keys - 1) / p.chunk_keys;
+  p.num_threads = chunks * p.waves_per_chunk * 64;
+  p.cw_level = a.cw_level;
+  p.cw_stride = a.cw_stride;
+  p.save = a.save_index != nullptr;
+  p.nl = a.nl;
+  p.b = a.b;
+  p.seeds_in = a.seeds_in;
+  p.ctrl_in = a.ctrl_in;
+  p.in_stride = a.in_stride;
+  p.parent = a.parent;
+  p.save_index = a.save_index;
+  p.seeds_out = a.seeds_out;
+  p.ctrl_out = a.ctrl_out;
+  p.out_stride = a.out_stride;
+  p.cw_seed = a.cw_seed;
+  p.cw_left = a.cw_left;
+  p.cw_right = a.cw_right;
+  p.vcw = a.vcw;
+  p.vcw_stride = a.vcw_stride;
+  p.party = a.party;
+  p.wide = a.wide;
+  p.leaf_seeds = a.leaf_seeds;
+  p.leaf_stride = a.leaf_stride;
+  for (int i = 0; i < a.nl; ++i) p.div[i] = make_div32(a.mod[i]);
+  p.rkl = expand_key(a.key_left);
+  p.rkr = expand_key(a.key_right);
+  p.rkv = expand_key(a.key_value);
+  int64_t grid = (p.num_threads + kHHBlock - 1) / kHHBlock;
+  if (grid > num_cus()) grid = num_cus();   // one 128 KiB-LDS workgroup per CU
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(hh_level_kernel, dim3((unsigned)grid), dim3(kHHBlock), 0, s, p);
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
+}  // namespace dpf_rt

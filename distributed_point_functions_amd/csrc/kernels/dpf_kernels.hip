@@ -22,8 +22,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+#include <map>
 #include <mutex>
 #include <type_traits>
 #include <thread>
@@ -784,7 +787,11 @@ constexpr size_t kBounceChunk = size_t{16} << 20;
 void host_copy(void* dst, const void* src, size_t bytes) {
   const size_t piece = size_t{2} << 20;
   size_t t = bytes / piece;
-  const size_t hw = std::thread::hardware_concurrency();
+  static const size_t hw = [] {
+    const char* e = std::getenv("DPF_HOST_THREADS");   // as host_util.h HostThreads()
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 ? static_cast<size_t>(v) : static_cast<size_t>(std::thread::hardware_concurrency());
+  }();
   if (t > 8) t = 8;
   if (hw && t > hw) t = hw;
   if (t <= 1) {
@@ -839,20 +846,75 @@ int bounce_d2h(void* dst, const void* src, size_t bytes, void* stream) {
 // and DMA straight into / out of it at the link rate (57 GB/s vs ~12 through
 // the bounce buffers); the bounce path stays as the fallback when the
 // registration is refused.
-constexpr size_t kRegisterMin = size_t{32} << 20;
+// Registering a fresh range (and unmapping it after) costs more than the
+// page-locked staging below ~0.5 GiB (tools/fresh_output_microbench.cc,
+// profiles/r14_fresh_output_microbench.jsonl): 32 MiB 4.5 vs 3.9 ms, 256 MiB
+// 26.3 vs 25.9 ms; at 8 GiB the DMA straight into the range wins (42 vs ~28 GB/s).
+constexpr size_t kRegisterMin = DPF_HIP_REGISTER_MIN_BYTES;
 constexpr size_t kStagedChunk = size_t{64} << 20;
 
-bool register_host(void* p, size_t bytes) {
-  if (hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess) return true;
-  (void)hipGetLastError();
-  return false;
+// The library's own transient registrations, reference-counted: a second
+// thread copying from or into a range another thread has registered for its
+// copy shares that registration (page_locked() would report the range as
+// page-locked and a plain async copy could outlive the first thread's
+// hipHostUnregister); the last user unregisters.  A request that overlaps a
+// registration without lying inside it takes the bounce path.
+struct Registration {
+  size_t bytes;
+  int users;
+};
+std::mutex g_reg_mu;
+std::map<uintptr_t, Registration> g_regs;   // base address -> registration
+std::atomic<int> g_reg_count{0};            // g_regs.size(), readable without the lock
+
+// Covers [p, p + bytes) with a library registration held by the caller (to be
+// released with release_host(*base)): an existing one that contains the range,
+// or -- for new ranges of >= kRegisterMin unless `reuse_only` -- a fresh one.
+enum Acquire { kNotOurs, kAcquired, kOverlaps };
+// kOverlaps: part of the range is in a registration of ours -- the copy must
+// take the bounce path (HIP would take the partly registered range as
+// page-locked).  kNotOurs: use the page-locked test / bounce path.
+Acquire acquire_host(void* p, size_t bytes, bool reuse_only, uintptr_t* base) {
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  auto it = g_regs.upper_bound(lo);
+  if (it != g_regs.begin()) {
+    auto prev = std::prev(it);
+    if (prev->first + prev->second.bytes > lo) {          // overlaps the one below
+      if (prev->first + prev->second.bytes >= hi) {        // contains the range
+        ++prev->second.users;
+        *base = prev->first;
+        return kAcquired;
+      }
+      return kOverlaps;
+    }
+  }
+  if (it != g_regs.end() && it->first < hi) return kOverlaps;  // overlaps the one above
+  if (reuse_only || bytes < kRegisterMin) return kNotOurs;
+  if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return kNotOurs;
+  }
+  g_regs[lo] = Registration{bytes, 1};
+  g_reg_count.store(static_cast<int>(g_regs.size()));
+  *base = lo;
+  return kAcquired;
+}
+
+void release_host(uintptr_t base) {
+  std::lock_guard<std::mutex> lock(g_reg_mu);
+  auto it = g_regs.find(base);
+  if (it == g_regs.end() || --it->second.users > 0) return;
+  (void)hipHostUnregister(reinterpret_cast<void*>(base));
+  g_regs.erase(it);
+  g_reg_count.store(static_cast<int>(g_regs.size()));
 }
 
 // Copies chunk by chunk on `s`, calling before(ctx, end) ahead of each chunk's
 // DMA (D2H: the destination chunk becomes valid while the previous chunk's
-// DMA runs).  `h` is registered by the caller.
+// DMA runs).  `h` lies in the registration acquired at `base`, released here.
 int registered_copy(char* h, char* d, size_t bytes, bool to_host, void (*before)(void*, size_t),
-                    void* ctx, hipStream_t s) {
+                    void* ctx, hipStream_t s, uintptr_t base) {
   int rc = kOk;
   for (size_t off = 0; off < bytes && rc == kOk; off += kStagedChunk) {
     const size_t len = bytes - off < kStagedChunk ? bytes - off : kStagedChunk;
@@ -863,7 +925,7 @@ int registered_copy(char* h, char* d, size_t bytes, bool to_host, void (*before)
   }
   const hipError_t e = hipStreamSynchronize(s);
   if (rc == kOk && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
-  (void)hipHostUnregister(h);
+  release_host(base);
   return rc;
 }
 
@@ -909,11 +971,16 @@ int dpf_hip_free(void* ptr) {
 }
 int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
   if (!bytes) return kOk;
-  if (bytes >= kBounceMin && !page_locked(src)) {
-    if (bytes >= kRegisterMin && register_host(const_cast<void*>(src), bytes))
+  uintptr_t base = 0;
+  if (bytes >= kBounceMin || g_reg_count.load() > 0) {
+    // Inside a registration of ours (another thread's copy), or large and new.
+    const Acquire a =
+        acquire_host(const_cast<void*>(src), bytes, bytes < kBounceMin || page_locked(src), &base);
+    if (a == kAcquired)
       return registered_copy((char*)const_cast<void*>(src), (char*)dst, bytes, false, nullptr,
-                             nullptr, (hipStream_t)stream);
-    return bounce_h2d(dst, src, bytes, stream);
+                             nullptr, (hipStream_t)stream, base);
+    if (a == kOverlaps || (bytes >= kBounceMin && !page_locked(src)))
+      return bounce_h2d(dst, src, bytes, stream);
   }
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -937,11 +1004,14 @@ int dpf_hip_memcpy_h2d_async(void* dst, const void* src, size_t bytes, void* str
 }
 int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
   if (!bytes) return kOk;
-  if (bytes >= kBounceMin && !page_locked(dst)) {
-    if (bytes >= kRegisterMin && register_host(dst, bytes))
+  uintptr_t base = 0;
+  if (bytes >= kBounceMin || g_reg_count.load() > 0) {
+    const Acquire a = acquire_host(dst, bytes, bytes < kBounceMin || page_locked(dst), &base);
+    if (a == kAcquired)
       return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, nullptr,
-                             nullptr, (hipStream_t)stream);
-    return bounce_d2h(dst, src, bytes, stream);
+                             nullptr, (hipStream_t)stream, base);
+    if (a == kOverlaps || (bytes >= kBounceMin && !page_locked(dst)))
+      return bounce_d2h(dst, src, bytes, stream);
   }
   HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
@@ -951,11 +1021,35 @@ int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
                               void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
                               void* stream) {
   if (!before_chunk) return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
-  if (bytes >= kRegisterMin && !page_locked(dst) && register_host(dst, bytes))
+  uintptr_t base = 0;
+  if (bytes >= kRegisterMin && acquire_host(dst, bytes, page_locked(dst), &base) == kAcquired)
     return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, before_chunk,
-                           ctx, (hipStream_t)stream);
+                           ctx, (hipStream_t)stream, base);
   before_chunk(ctx, bytes);
   return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
+}
+int dpf_hip_memcpy_d2h_chunked(const void* src, size_t bytes, size_t align,
+                               void (*consume)(void* ctx, const void* chunk, size_t offset,
+                                               size_t len),
+                               void* ctx, void* stream) {
+  if (!bytes) return kOk;
+  if (!src || !consume || align == 0 || align > kBounceChunk)
+    return fail(kInvalidArgument, "dpf_hip_memcpy_d2h_chunked: bad arguments");
+  std::lock_guard<std::mutex> lock(g_bounce_mu);
+  if (int rc = bounce_buffers()) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t chunk = kBounceChunk / align * align;
+  const size_t n = (bytes + chunk - 1) / chunk;
+  auto len = [&](size_t i) { return i + 1 < n ? chunk : bytes - i * chunk; };
+  HIP_TRY(hipMemcpyAsync(g_bounce[0], src, len(0), hipMemcpyDeviceToHost, s));
+  for (size_t i = 0; i < n; ++i) {
+    HIP_TRY(hipStreamSynchronize(s));   // chunk i is in g_bounce[i & 1]
+    if (i + 1 < n)
+      HIP_TRY(hipMemcpyAsync(g_bounce[(i + 1) & 1], (const char*)src + (i + 1) * chunk, len(i + 1),
+                             hipMemcpyDeviceToHost, s));
+    consume(ctx, g_bounce[i & 1], i * chunk, len(i));
+  }
+  return kOk;
 }
 int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
   if (!bytes) return kOk;

@@ -26,6 +26,37 @@ int validate_desc(const dpf_value_desc* d);    // kOk or the failure code
 int packed_size(const dpf_value_desc* d);      // bytes of one packed element
 bool fast_int(const dpf_value_desc* d);        // one plain/XOR integer leaf, direct, b == 1
 
+// One steady-state heavy-hitters level (dpf_batch_hh.hip): start seeds from
+// the expansion cache or gathered partial evaluations, no path walk, two
+// expanded levels, Tuple/IntModN<uint32_t> values summed over the keys.
+struct HHLevelArgs {
+  int64_t num_keys, num_starts;
+  int cw_level, cw_stride;
+  const dpf_block* seeds_in;
+  const uint8_t* ctrl_in;    // NULL: control bit in bit 0 of the seed
+  int64_t in_stride;
+  const int32_t* parent;
+  const int32_t* save_index;  // NULL: no partial evaluations stored
+  dpf_block* seeds_out;
+  uint8_t* ctrl_out;
+  int64_t out_stride;
+  const dpf_block* cw_seed;
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  const dpf_block* vcw;
+  int vcw_stride;
+  const uint8_t* party;
+  unsigned long long* wide;
+  dpf_block* leaf_seeds;
+  int64_t leaf_stride;
+  int nl, b;
+  uint32_t mod[2];
+  const dpf_aes_key* key_left;
+  const dpf_aes_key* key_right;
+  const dpf_aes_key* key_value;
+};
+int launch_hh_level(const HHLevelArgs& a, hipStream_t s);
+
 }  // namespace dpf_rt
 
 #define HIP_TRY(expr)                                           \

@@ -76,6 +76,8 @@ def load(require_gpu: bool = False):
         L.dpf_hip_last_error.restype = ctypes.c_char_p
         L.dpf_hip_last_expand_kernel.restype = ctypes.c_char_p
         L.dpf_hip_last_expand_kernel.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.dpf_hip_last_batch_kernel.restype = ctypes.c_char_p
+        L.dpf_hip_last_batch_kernel.argtypes = []
         L.dpf_hip_hash.argtypes = [I64, P, P, P, P]
         L.dpf_hip_eval_paths.argtypes = [I64, I, P, P, P, P, P, P, P, P, P, P, P]
         L.dpf_hip_expand.argtypes = [I64, P, P, I, P, P, P, P, P, P, P, I, P, I, P, P]
@@ -103,6 +105,12 @@ def last_expand_kernel():
     d = ctypes.c_int(-1)
     name = load().dpf_hip_last_expand_kernel(ctypes.byref(d)).decode()
     return name, d.value
+
+
+def last_batch_kernel() -> str:
+    """Kernel of this thread's last batched prefix evaluation, e.g. "hh_level"
+    -- dispatch diagnostics for the tests."""
+    return load().dpf_hip_last_batch_kernel().decode()
 
 
 def check(st: int):

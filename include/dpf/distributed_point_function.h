@@ -159,10 +159,14 @@ class DistributedPointFunction {
       if (!status.ok()) return status;
       return out;
     } else {
-      StatusOr<std::vector<uint8_t>> packed =
-          EvaluateUntilPacked(hierarchy_level, prefixes, ctx, &t);
-      if (!packed.ok()) return packed.status();
-      return Unpack<T>(hierarchy_level, *packed);
+      // Packed tuples / IntModN / XorWrapper values are unpacked straight out
+      // of the page-locked staging buffers into the result, chunk by chunk
+      // (the sink reads flat_[hierarchy_level] only after validation).
+      std::vector<T> out;
+      const HostSink sink = dpf_internal::UnpackSink(&flat_, hierarchy_level, &out);
+      Status status = EvaluateUntilToHost(hierarchy_level, prefixes, ctx, &t, sink);
+      if (!status.ok()) return status;
+      return out;
     }
   }
 

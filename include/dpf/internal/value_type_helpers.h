@@ -285,27 +285,88 @@ std::vector<T> MakeOutputVector(int64_t n) {
 }
 
 // Where a packed device output is copied on the host (EvaluateUntilToHost):
-// reserve(bytes) returns storage for it; grow(bytes) (may be empty) makes its
-// first `bytes` bytes valid and is called chunk by chunk right before each
-// chunk's DMA, so a fresh vector's value-initialisation overlaps the copy
-// (dpf_hip_memcpy_d2h_staged).
+// reserve(bytes) returns storage for it (or nullptr when the sink takes the
+// bytes chunk by chunk); grow(bytes) (may be empty) makes its first `bytes`
+// bytes valid and is called chunk by chunk right before each chunk's DMA, so a
+// fresh vector's value-initialisation overlaps the copy
+// (dpf_hip_memcpy_d2h_staged).  chunk(bytes, offset, len) (may be empty)
+// receives [offset, offset + len) of the packed output from page-locked
+// staging while the next chunk's DMA runs (dpf_hip_memcpy_d2h_chunked; len
+// and offset multiples of `align`): used for every output below
+// DPF_HIP_REGISTER_MIN_BYTES and whenever reserve() returned nullptr.
 struct HostSink {
   std::function<void*(size_t bytes)> reserve;
   std::function<void(size_t bytes)> grow;
+  std::function<void(const uint8_t* bytes, size_t offset, size_t len)> chunk;
+  size_t align = 1;
 };
+
+// fn(lo, hi) over [0, n) in chunks of at least `grain`, on up to 16 host threads.
+void ParallelRanges(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn);
 
 // The HostSink that fills a fresh std::vector<T> (bytes: a multiple of sizeof(T)).
 template <typename T>
 HostSink VectorSink(std::vector<T>* out) {
-  return HostSink{[out](size_t bytes) -> void* {
-                    ReserveOutputVector(*out, static_cast<int64_t>(bytes / sizeof(T)));
-                    return out->data();
-                  },
-                  [out](size_t bytes) { out->resize((bytes + sizeof(T) - 1) / sizeof(T)); }};
+  HostSink s;
+  s.reserve = [out](size_t bytes) -> void* {
+    ReserveOutputVector(*out, static_cast<int64_t>(bytes / sizeof(T)));
+    return out->data();
+  };
+  s.grow = [out](size_t bytes) { out->resize((bytes + sizeof(T) - 1) / sizeof(T)); };
+  s.chunk = [out](const uint8_t* src, size_t offset, size_t len) {
+    out->resize((offset + len) / sizeof(T));
+    uint8_t* dst = reinterpret_cast<uint8_t*>(out->data()) + offset;
+    ParallelRanges(static_cast<int64_t>(len), int64_t{2} << 20, [&](int64_t lo, int64_t hi) {
+      std::memcpy(dst + lo, src + lo, static_cast<size_t>(hi - lo));
+    });
+  };
+  s.align = sizeof(T);
+  return s;
 }
 
-// fn(lo, hi) over [0, n) in chunks of at least `grain`, on up to 16 host threads.
-void ParallelRanges(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn);
+// Unpacks n packed elements of T into out[0, n) (value_type_helpers.h:526-589:
+// the packed image is the kernels' little-endian leaf concatenation).
+template <typename T>
+void UnpackInto(const FlatValueType& flat, const uint8_t* data, int64_t n, T* out) {
+  if (flat.packed_size == ValueTypeHelper<T>::kPackedBytes) {
+    // The packed layout of T is known at compile time: fixed-width loads of
+    // each leaf straight into the element (no per-leaf uint128 round trip).
+    const int step = flat.packed_size;
+    ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i) out[i] = ValueTypeHelper<T>::FromPacked(data + i * step);
+    });
+    return;
+  }
+  ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
+    std::vector<uint128> leaves(flat.leaves.size());
+    for (int64_t i = lo; i < hi; ++i) {
+      UnpackLeaves(flat, data + i * flat.packed_size, leaves.data());
+      out[i] = ValueTypeHelper<T>::FromLeaves(leaves.data());
+    }
+  });
+}
+
+// The HostSink that unpacks packed elements of T into a fresh std::vector<T>
+// chunk by chunk, straight out of page-locked staging (no host copy of the
+// packed bytes).
+template <typename T>
+HostSink UnpackSink(const std::vector<FlatValueType>* flats, int h, std::vector<T>* out) {
+  HostSink s;
+  s.reserve = [flats, h, out](size_t bytes) -> void* {
+    ReserveOutputVector(*out, static_cast<int64_t>(bytes / (*flats)[h].packed_size));
+    return nullptr;
+  };
+  s.chunk = [flats, h, out](const uint8_t* src, size_t offset, size_t len) {
+    const FlatValueType& flat = (*flats)[h];
+    const int64_t first = static_cast<int64_t>(offset / flat.packed_size);
+    const int64_t cnt = static_cast<int64_t>(len / flat.packed_size);
+    out->resize(first + cnt);
+    UnpackInto<T>(flat, src, cnt, out->data() + first);
+  };
+  // Valid levels only (the sink is used after validation); 1 otherwise.
+  s.align = h >= 0 && h < static_cast<int>(flats->size()) ? (*flats)[h].packed_size : 1;
+  return s;
+}
 
 // Unpacks n packed elements of T.
 template <typename T>
@@ -319,22 +380,7 @@ std::vector<T> UnpackElements(const FlatValueType& flat, const uint8_t* data, in
     }
   }
   std::vector<T> out = MakeOutputVector<T>(n);
-  if (flat.packed_size == ValueTypeHelper<T>::kPackedBytes) {
-    // The packed layout of T is known at compile time: fixed-width loads of
-    // each leaf straight into the element (no per-leaf uint128 round trip).
-    const int step = flat.packed_size;
-    ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
-      for (int64_t i = lo; i < hi; ++i) out[i] = ValueTypeHelper<T>::FromPacked(data + i * step);
-    });
-    return out;
-  }
-  ParallelRanges(n, int64_t{1} << 15, [&](int64_t lo, int64_t hi) {
-    std::vector<uint128> leaves(flat.leaves.size());
-    for (int64_t i = lo; i < hi; ++i) {
-      UnpackLeaves(flat, data + i * flat.packed_size, leaves.data());
-      out[i] = ValueTypeHelper<T>::FromLeaves(leaves.data());
-    }
-  });
+  UnpackInto<T>(flat, data, n, out.data());
   return out;
 }
 

@@ -103,22 +103,45 @@ class DeviceBatchContext {
   // Device arrays [num_keys][partial_prefixes().size()].
   const dpf_block* partial_seeds() const { return static_cast<const dpf_block*>(seeds_); }
   const uint8_t* partial_control() const { return static_cast<const uint8_t*>(ctrl_); }
-  // Back to the state CreateBatchEvaluationContext returns, keeping the device
-  // allocations for the next pass over the hierarchy.
-  void Reset() {
-    previous_hierarchy_level_ = -1;
-    partial_evaluations_level_ = -1;
-    partial_prefixes_.clear();
-    leaf_level_ = -1;
-  }
+  // Back to the state CreateBatchEvaluationContext returns, keeping the
+  // per-call device allocations for the next pass over the hierarchy; the
+  // expansion cache (up to K x 4096 x 16 B) is released.
+  void Reset();
   // Hierarchy level whose call wrote the expansion cache (-1: none).
   int expansion_cache_level() const { return leaf_level_; }
+  // Device bytes this context holds (partial evaluations, expansion cache,
+  // per-call scratch).
+  size_t device_bytes() const { return device_bytes_; }
+  // What the expansion cache did under memory pressure, since creation.
+  struct CacheEvents {
+    int64_t cache_refused = 0;   // no room for the cache: the call wrote none
+    int64_t spare_refused = 0;   // no room for a spare: start seeds gathered, cache rewritten in place
+    int64_t in_place = 0;        // calls that took the gather + in-place path
+    int64_t evicted_spare = 0;   // spare freed so a per-call buffer fits
+    int64_t evicted_cache = 0;   // unread cache freed so a per-call buffer fits
+    int64_t alloc_failures = 0;  // per-call allocations that failed (before any eviction)
+  };
+  const CacheEvents& cache_events() const { return events_; }
+  // Test hook: after `skip` more per-call buffer requests, the next n fail as
+  // if the device were out of memory (whether or not the buffer has to grow).
+  void FailNextAllocationsForTesting(int n, int skip = 0) {
+    fail_next_ = n;
+    fail_skip_ = skip;
+  }
 
  private:
   friend class DistributedPointFunction;
   explicit DeviceBatchContext(const DeviceKeyBatch* keys) : keys_(keys) {}
-  // Grows a device allocation (contents are not preserved).
-  static Status Ensure(void** p, size_t* cap, size_t bytes);
+  // Grows a device allocation (contents are not preserved).  Failures are
+  // RESOURCE_EXHAUSTED "Memory allocation error" (distributed_point_function.cc:289-291).
+  Status Ensure(void** p, size_t* cap, size_t bytes);
+  // Allocates exactly `bytes` into *p (*p must be null); false on failure.
+  bool TryAlloc(void** p, size_t* cap, size_t bytes);
+  void Release(void** p, size_t* cap);
+  // Free and total device memory as this context sees it (DPF_BATCH_ALLOC_LIMIT
+  // replaces the device's figures with the limit, as a test hook).
+  void MemInfo(size_t* free_bytes, size_t* total_bytes) const;
+  void ReleaseExpansionCache();
 
   const DeviceKeyBatch* keys_;
   int previous_hierarchy_level_ = -1;
@@ -148,6 +171,9 @@ class DeviceBatchContext {
   int leaf_de_ = 0;
   void* slots_ = nullptr;
   size_t slots_cap_ = 0;
+  size_t device_bytes_ = 0;  // sum of the caps below and above
+  CacheEvents events_;
+  int fail_next_ = 0, fail_skip_ = 0;
   // Per-call scratch: start-node tables, sums workspace, staging output.
   void* parent_ = nullptr;
   void* path_ = nullptr;

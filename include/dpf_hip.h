@@ -99,6 +99,21 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
  * initialisation of the next.  Large copies DMA straight into `dst`
  * (registered for the copy), others go through page-locked staging.  The
  * drop-in EvaluateUntil<T> returns its std::vector<T> this way. */
+/* Host ranges of at least this many bytes are registered (page-locked) for a
+ * copy and DMAed straight into; smaller ones go through page-locked staging. */
+#define DPF_HIP_REGISTER_MIN_BYTES ((size_t)512 << 20)
+
+/* D2H copy handed to the host chunk by chunk: the bytes arrive in the
+ * library's page-locked staging buffers, and `consume(ctx, chunk, offset,
+ * len)` gets [offset, offset + len) of the source (len a multiple of `align`,
+ * <= 16 MiB) while the next chunk's DMA runs.  Returns after the last
+ * consume.  The drop-in EvaluateUntil<T> unpacks packed tuples / IntModN
+ * values straight into its result vector this way (no host copy of the packed
+ * bytes), and mid-sized integer outputs are copied into theirs. */
+int dpf_hip_memcpy_d2h_chunked(const void* src, size_t bytes, size_t align,
+                               void (*consume)(void* ctx, const void* chunk, size_t offset,
+                                               size_t len),
+                               void* ctx, void* stream);
 int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
                               void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
                               void* stream);
@@ -157,6 +172,13 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
  * generic; "" before the first call), and the depth-first subtree depth it
  * chose.  Tests use it to pin the dispatch. */
 const char* dpf_hip_last_expand_kernel(int* subtree_depth);
+
+/* Diagnostic: which kernel the calling thread's last
+ * dpf_hip_eval_prefix_batch(_cached) launched: "hh_level" (the lean
+ * heavy-hitters kernel: cached or gathered start seeds, two expanded levels,
+ * IntModN<uint32_t> sums), "batch_level/fast", "batch_level/mod32" or
+ * "batch_level/generic"; "" before the first call. */
+const char* dpf_hip_last_batch_kernel(void);
 
 /* ---- a11: fused point evaluation for many keys ----------------------------
  * Replaces EvaluateAtImpl's path walk + hash + correction (h:930-1003).

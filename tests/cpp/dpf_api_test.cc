@@ -59,6 +59,8 @@ template <> dpf::XorWrapper<uint128> Beta<dpf::XorWrapper<uint128>>() {
 template <> dpf::Tuple<uint32_t, uint64_t> Beta<dpf::Tuple<uint32_t, uint64_t>>() {
   return dpf::Tuple<uint32_t, uint64_t>(0x11223344u, 0x5566778899AABBCCull);
 }
+using U32x5 = dpf::Tuple<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>;
+template <> U32x5 Beta<U32x5>() { return U32x5(1u, 0xFFFFFFFFu, 3u, 0x80000000u, 5u); }
 template <> dpf::Tuple<ModN32, ModN32> Beta<dpf::Tuple<ModN32, ModN32>>() {
   return dpf::Tuple<ModN32, ModN32>(ModN32(123456789u), ModN32(4000000000u));
 }
@@ -231,6 +233,13 @@ int main() {
   FullDomain<uint64_t>("uint64_t", 23);
   FullDomain<dpf::Tuple<uint32_t, uint64_t>>("Tuple<uint32_t, uint64_t>", 22);
   FullDomain<dpf::Tuple<ModN64, ModN64, ModN64>>("Tuple<IntModN64 x3>", 10);
+  // Chunked unpacking out of the 16 MiB staging buffers (chunks that are not
+  // a power of two: 20- and 12-byte packed elements), and the registered DMA
+  // straight into a 512 MiB result vector.
+  FullDomain<U32x5>("Tuple<uint32_t x5>", 20);
+  FullDomain<dpf::Tuple<uint32_t, uint64_t>>("Tuple<uint32_t, uint64_t>", 23);
+  FullDomain<dpf::Tuple<ModN32, ModN32>>("Tuple<IntModN32 x2>", 22);
+  FullDomain<uint64_t>("uint64_t", 26);
   Hierarchical();
   DeviceRetryAfterSmallBuffer();
   for (int log : {3, 16, 64}) {

@@ -362,13 +362,15 @@ def test_evaluate_shard_to_device_errors():
         dpf2.evaluate_shard_to_device(1, 0, 2, ctx, dev)
 
 
-@pytest.mark.parametrize("log,vt", [(26, ("int", 64)), (25, ("int", 128)),
+@pytest.mark.parametrize("log,vt", [(26, ("int", 64)), (25, ("int", 128)), (22, ("int", 64)),
                                     (24, ("tuple", [("int", 32), ("int", 64)]))], ids=str)
 def test_large_host_output_matches_device(log, vt):
-    """Host outputs of >= 32 MiB take dpf_hip_memcpy_d2h_staged: the fresh
-    vector is registered and value-initialised chunk by chunk while the
-    previous 64 MiB chunk's DMA runs.  Every byte equals the device output,
-    and the two parties' host outputs reconstruct the point function."""
+    """Host outputs of >= 512 MiB (DPF_HIP_REGISTER_MIN_BYTES) take
+    dpf_hip_memcpy_d2h_staged: the fresh vector is registered and
+    value-initialised chunk by chunk while the previous 64 MiB chunk's DMA
+    runs; smaller ones arrive through the 16 MiB page-locked staging buffers
+    chunk by chunk (dpf_hip_memcpy_d2h_chunked).  Every byte equals the device
+    output, and the two parties' host outputs reconstruct the point function."""
     import torch
     dpf = E.params([(log, vt, 0)])
     alpha = (1 << log) - 12345

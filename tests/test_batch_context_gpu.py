@@ -209,3 +209,180 @@ def test_batch_errors_match_reference():
         dpf.evaluate_until_batch_to_device(2, [200], bctx, out)
     with pytest.raises(D.DpfStatusError, match="device output buffer too small"):
         dpf.evaluate_until_batch_to_device(2, [3 << 4], bctx, out[:10])
+
+
+# ---------------------------------------------------------------------------
+# The expansion cache under memory pressure (batch_context.cc: the spare and
+# cache allocations, the per-call buffers' eviction-and-retry).  Whatever the
+# cache does, outputs and exported contexts must equal the oracle's; a call
+# that cannot get its per-call buffers fails with the reference's
+# RESOURCE_EXHAUSTED "Memory allocation error" (distributed_point_function.cc:
+# 289-291) and leaves the context usable: the same call retried succeeds.
+# ---------------------------------------------------------------------------
+
+def _pressure_run(levels, plan, n_keys, sum_mode, seed, arm=None, limit=None, monkeypatch=None):
+    """Like _run; arm(i, bctx) is called before call i (it may arm the
+    fail-next-allocations hook).  With `limit`, DPF_BATCH_ALLOC_LIMIT is set
+    for every call.  A call failing with RESOURCE_EXHAUSTED is retried once
+    with the hooks off.  Returns (bctx, indices of calls that failed,
+    device_bytes after each call)."""
+    import torch
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=seed, party_mix=True)
+    bctx = dpf.create_batch_evaluation_context(dpf.upload_key_batch(batch))
+    octx = [O.create_context(P, k) for k in oks]
+    failed, held = [], []
+    for i, (h, prefixes) in enumerate(_prefix_plan(P, plan, rng)):
+        size = dpf.packed_size(h)
+        n_out = dpf.output_elements(h, len(prefixes), bctx.previous_hierarchy_level)
+        rows = 1 if sum_mode else n_keys
+        out = torch.full((rows * n_out * size,), 0xAB, dtype=torch.uint8, device="cuda")
+        if arm:
+            arm(i, bctx)
+        if limit is not None:
+            monkeypatch.setenv("DPF_BATCH_ALLOC_LIMIT", str(limit))
+        try:
+            n = dpf.evaluate_until_batch_to_device(h, prefixes, bctx, out, sum_over_keys=sum_mode)
+        except D.DpfStatusError as e:
+            assert "RESOURCE_EXHAUSTED" in str(e) and "Memory allocation error" in str(e), str(e)
+            failed.append(i)
+            bctx.fail_next_allocations_for_testing(0)
+            if limit is not None:
+                monkeypatch.delenv("DPF_BATCH_ALLOC_LIMIT")
+            assert bctx.previous_hierarchy_level != h   # the failed call left ctx as it was
+            n = dpf.evaluate_until_batch_to_device(h, prefixes, bctx, out, sum_over_keys=sum_mode)
+        finally:
+            if limit is not None:
+                monkeypatch.delenv("DPF_BATCH_ALLOC_LIMIT", raising=False)
+        torch.cuda.synchronize()
+        assert n == n_out
+        got = out.cpu().numpy().reshape(rows, n_out, size)
+        want = [O.evaluate_until(P, h, prefixes, c) for c in octx]
+        if sum_mode:
+            acc = want[0]
+            for w in want[1:]:
+                acc = O.add_packed(levels[h][1], acc, w)
+            np.testing.assert_array_equal(got[0], acc, err_msg=f"call {i} level {h}")
+        else:
+            for k in range(n_keys):
+                np.testing.assert_array_equal(got[k], want[k], err_msg=f"call {i} level {h} key {k}")
+        held.append(bctx.device_bytes)
+        _check_export(dpf, bctx, batch, octx, n_keys - 1)
+    return bctx, failed, held
+
+
+HH5 = CASES[0]   # Tuple<IntModN32 x2>, five levels, 2-bit steps
+
+
+@pytest.mark.parametrize("sum_mode", [False, True])
+def test_cache_spare_evicted_for_per_call_buffer(sum_mode):
+    """Call 2 reads the cache and would write the spare; its first per-call
+    allocation fails once, so the spare is freed, the call writes no cache,
+    and call 3 walks down from the partial evaluations and rebuilds it."""
+    levels, plan = HH5
+    arm = lambda i, c: c.fail_next_allocations_for_testing(1) if i == 2 else None
+    bctx, failed, held = _pressure_run(levels, plan, 33, sum_mode, seed=91, arm=arm)
+    ev = bctx.cache_events
+    assert failed == [] and ev["evicted_spare"] == 1 and ev["evicted_cache"] == 0, ev
+    assert ev["alloc_failures"] == 1, ev
+    # After the last level the cache is released: nothing but per-call state.
+    assert bctx.expansion_cache_level == -1
+    assert held[-1] < max(held)
+
+
+@pytest.mark.parametrize("sum_mode", [False, True])
+def test_cache_in_use_cannot_be_evicted_call_fails_and_retries(sum_mode):
+    """Call 3 reads the cache; two allocation failures free the spare and then
+    find only the cache the call is reading: RESOURCE_EXHAUSTED.  The same
+    call retried reads the still-valid cache and succeeds."""
+    levels, plan = HH5
+    arm = lambda i, c: c.fail_next_allocations_for_testing(2) if i == 3 else None
+    bctx, failed, _ = _pressure_run(levels, plan, 21, sum_mode, seed=92, arm=arm)
+    ev = bctx.cache_events
+    assert failed == [3] and ev["evicted_spare"] == 1 and ev["evicted_cache"] == 0, ev
+
+
+def test_cache_evicted_after_in_place_gather(monkeypatch):
+    """No spare (the in-place path): once call 2 has gathered its start seeds
+    the cache is only the write target, so a per-call allocation failure after
+    the gather frees it -- the call writes no cache, call 3 walks down from
+    the partial evaluations and rebuilds it."""
+    monkeypatch.setenv("DPF_BATCH_CACHE_IN_PLACE", "1")
+    levels, plan = HH5
+    # Six per-call buffers precede the gather (parent/path/save tables, the
+    # next partial evaluations' seeds and control bits, the cache slots).
+    arm = lambda i, c: c.fail_next_allocations_for_testing(1, skip=6) if i == 2 else None
+    bctx, failed, _ = _pressure_run(levels, plan, 17, True, seed=93, arm=arm)
+    ev = bctx.cache_events
+    assert failed == [] and ev["evicted_cache"] == 1 and ev["evicted_spare"] == 0, ev
+    assert ev["in_place"] >= 2, ev
+
+
+@pytest.mark.parametrize("frac", [0.9, 0.7, 0.5, 0.35])
+def test_cache_under_device_memory_limit(frac, monkeypatch):
+    """DPF_BATCH_ALLOC_LIMIT models a device with less memory: below the
+    unlimited run's peak the spare (quarter-of-device headroom) and then the
+    cache (an eighth) are refused or evicted; calls that cannot get their
+    per-call buffers fail with RESOURCE_EXHAUSTED and succeed on retry."""
+    levels, plan = HH5
+    bctx0, _, held0 = _pressure_run(levels, plan, 64, True, seed=94)
+    limit = int(max(held0) * frac)
+    bctx, failed, _ = _pressure_run(levels, plan, 64, True, seed=94, limit=limit,
+                                    monkeypatch=monkeypatch)
+    ev = bctx.cache_events
+    assert ev["spare_refused"] + ev["cache_refused"] + ev["evicted_spare"] + ev["evicted_cache"] \
+        + len(failed) > 0, ev
+
+
+def test_allocation_limit_too_small_is_resource_exhausted(monkeypatch):
+    """A limit below the first call's per-call buffers (one byte): the
+    reference's RESOURCE_EXHAUSTED message, and the context is untouched."""
+    import torch
+    levels, plan = HH5
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, 8, seed=95)
+    bctx = dpf.create_batch_evaluation_context(dpf.upload_key_batch(batch))
+    out = torch.empty(1 << 16, dtype=torch.uint8, device="cuda")
+    monkeypatch.setenv("DPF_BATCH_ALLOC_LIMIT", "1")
+    with pytest.raises(D.DpfStatusError, match="Memory allocation error"):
+        dpf.evaluate_until_batch_to_device(0, [], bctx, out)
+    assert bctx.previous_hierarchy_level == -1
+    monkeypatch.delenv("DPF_BATCH_ALLOC_LIMIT")
+    dpf.evaluate_until_batch_to_device(0, [], bctx, out)
+    assert bctx.previous_hierarchy_level == 0
+
+
+def test_reset_releases_expansion_cache():
+    """Reset() gives the expansion cache's memory back."""
+    import torch
+    levels, plan = HH5
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, 40, seed=96)
+    bctx = dpf.create_batch_evaluation_context(dpf.upload_key_batch(batch))
+    out = torch.empty(40 * (1 << 12) * 8, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_until_batch_to_device(0, [], bctx, out)
+    dpf.evaluate_until_batch_to_device(1, [0, 1, 5], bctx, out)
+    torch.cuda.synchronize()
+    assert bctx.expansion_cache_level == 1
+    before = bctx.device_bytes
+    bctx.reset()
+    assert bctx.expansion_cache_level == -1 and bctx.device_bytes < before
+    dpf.evaluate_until_batch_to_device(0, [], bctx, out)
+    assert bctx.expansion_cache_level == 0
+
+
+def test_heavy_hitters_levels_run_the_lean_kernel(monkeypatch):
+    """Cached heavy-hitters levels (start seeds from the expansion cache, two
+    expanded levels, Tuple<IntModN32 x2> sums) run hh_level_kernel
+    (dpf_batch_hh.hip); DPF_BATCH_NO_LEAN=1 runs the general kernel.  Both
+    equal the oracle (checked by _run), and each other."""
+    from distributed_point_functions_amd import hip_abi as H
+    levels, plan = HH5
+    seen = []
+
+    def arm(i, c):
+        if i > 0:
+            seen.append(H.last_batch_kernel())
+    _pressure_run(levels, plan, 45, True, seed=97, arm=arm)
+    seen.append(H.last_batch_kernel())
+    assert seen[-1] == "hh_level", seen   # the last (cached) level
+    monkeypatch.setenv("DPF_BATCH_NO_LEAN", "1")
+    _pressure_run(levels, plan, 45, True, seed=97)
+    assert H.last_batch_kernel() == "batch_level/mod32"

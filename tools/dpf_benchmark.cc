@@ -59,6 +59,7 @@ struct Row {
 struct Runner {
   std::regex filter{".*"};
   double min_time = 0.2;
+  bool split = false;   // --split: per-phase times of BM_EvaluateRegularDpf instead
   std::vector<Row> rows;
 
   // `body(n)` runs n timed iterations; `label` is printed after the time.
@@ -116,6 +117,55 @@ std::string Rate(double items, const char* unit, double secs) {
   return buf;
 }
 
+// --split: where one EvaluateNext<T>({}) call's time goes on the host, median
+// of 30 calls: the context copy, the packed evaluation (kernel + D2H into a
+// fresh byte vector), the unpack into a fresh std::vector<T>, and freeing both;
+// and the whole EvaluateNext<T> call as the benchmark makes it.
+template <typename T>
+void SplitPhases(const DistributedPointFunction& f, const EvaluationContext& ctx0,
+                 const std::string& name) {
+  using clk = std::chrono::steady_clock;
+  auto secs = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  const std::vector<uint128> none;
+  const dpf::ValueType t = dpf::ToValueType<T>();
+  constexpr int kReps = 30;
+  std::vector<double> ph[5];
+  for (int i = 0; i < kReps + 2; ++i) {
+    auto t0 = clk::now();
+    EvaluationContext ctx = ctx0;
+    auto t1 = clk::now();
+    std::vector<uint8_t> packed = Must(f.EvaluateUntilPacked(0, none, ctx, &t), "packed");
+    auto t2 = clk::now();
+    std::vector<T> out = dpf::dpf_internal::UnpackElements<T>(
+        f.flat_value_type(0), packed.data(), static_cast<int64_t>(packed.size() /
+                                                               f.flat_value_type(0).packed_size));
+    auto t3 = clk::now();
+    Sink(out);
+    { std::vector<uint8_t>().swap(packed); std::vector<T>().swap(out); }
+    auto t4 = clk::now();
+    EvaluationContext ctx2 = ctx0;
+    Sink(Must(f.template EvaluateNext<T>(none, ctx2), "EvaluateNext"));
+    auto t5 = clk::now();
+    if (i < 2) continue;
+    ph[0].push_back(secs(t0, t1));
+    ph[1].push_back(secs(t1, t2));
+    ph[2].push_back(secs(t2, t3));
+    ph[3].push_back(secs(t3, t4));
+    ph[4].push_back(secs(t4, t5));
+  }
+  auto med = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2] * 1e3;
+  };
+  auto mx = [](const std::vector<double>& v) { return *std::max_element(v.begin(), v.end()) * 1e3; };
+  std::printf("%-72s ctx %.3f  packed %.3f  unpack %.3f  free %.3f  | EvaluateNext %.3f "
+              "(max %.3f) ms\n", name.c_str(), med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]),
+              med(ph[4]), mx(ph[4]));
+  std::fflush(stdout);
+}
+
 // ---------------------------------------------------------------------------
 // BM_EvaluateRegularDpf<T>/log: EvaluateNext<T>({}) on a fresh copy of a
 // single-level context (reference benchmark.cc:27-49), alpha = 0, beta = T{}.
@@ -133,6 +183,10 @@ void EvaluateRegularDpf(Runner& r, const std::string& tname, int lo, int hi) {
     auto keys = Must(f->GenerateKeys(uint128{0}, T{}), "GenerateKeys");
     const EvaluationContext ctx0 = Must(f->CreateEvaluationContext(keys.first), "ctx");
     const std::vector<uint128> none;
+    if (r.split) {
+      SplitPhases<T>(*f, ctx0, name);
+      continue;
+    }
     r.Run(name, [&](int64_t n) {
       for (int64_t i = 0; i < n; ++i) {
         EvaluationContext ctx = ctx0;
@@ -371,8 +425,9 @@ int main(int argc, char** argv) {
     if (const char* v = val("--benchmark_filter=")) r.filter = std::regex(v);
     else if (const char* v = val("--benchmark_min_time=")) r.min_time = std::atof(v);
     else if (const char* v = val("--json=")) json = v;
+    else if (a == "--split") r.split = true;
     else {
-      std::fprintf(stderr, "usage: %s [--benchmark_filter=RE] [--benchmark_min_time=S] [--json=PATH]\n",
+      std::fprintf(stderr, "usage: %s [--benchmark_filter=RE] [--benchmark_min_time=S] [--json=PATH] [--split]\n",
                    argv[0]);
       return 2;
     }

@@ -7,6 +7,12 @@ fraction, VALU / LDS instructions per AES block and HBM write bytes (WRITE_SIZE
 is in KiB on gfx950, MI355X_MICROARCH.md; GRBM_GUI_ACTIVE sums the 8 XCDs).
 
   python tools/pmc_summary.py <dir> <kernel substring> --aes N --bytes B [--tag t]
+  python tools/pmc_summary.py <dir> <kernel substring> --bench-log <trace pass log> \
+      --workload <bench.py workload tag> [--skip W | --total --passes P]
+
+--bench-log takes the algorithmic AES / bytes / outputs per launch (or per
+pass) from the bench.py JSON line the profiled command printed, and
+--workload tags the summary so bench.py quotes it for that workload only.
 """
 import argparse
 import csv
@@ -22,8 +28,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("kernel")
-    ap.add_argument("--aes", type=int, required=True, help="algorithmic AES blocks per launch")
-    ap.add_argument("--bytes", type=int, required=True, help="algorithmic bytes written per launch")
+    ap.add_argument("--aes", type=int, default=None, help="algorithmic AES blocks per launch")
+    ap.add_argument("--bytes", type=int, default=None, help="algorithmic bytes written per launch")
+    ap.add_argument("--bench-log", default=None,
+                    help="log of the profiled bench.py run: its JSON line supplies --aes/--bytes/--leaves")
+    ap.add_argument("--workload", default=None, help="bench.py workload tag this summary is for")
+    ap.add_argument("--passes", type=int, default=1,
+                    help="--total mode: the profiled run repeated the workload this many times "
+                         "(warmup + timed steps); totals are divided by it")
     ap.add_argument("--tag", default="")
     ap.add_argument("--total", action="store_true",
                     help="sum every matching dispatch (a workload of many differently sized "
@@ -34,7 +46,28 @@ def main():
     ap.add_argument("--leaves", type=int, default=None,
                     help="outputs per launch (full domain; bench.py's profiled_traffic key)")
     a = ap.parse_args()
+    a.kernel = a.kernel.replace("(anonymous namespace)::", "")
     res = {"tag": a.tag}
+    if a.workload:
+        res["workload"] = a.workload
+    if a.bench_log:
+        line = None
+        for ln in open(a.bench_log, errors="replace"):
+            if ln.startswith("{") and '"metric"' in ln:
+                line = json.loads(ln)
+        if line is None:
+            raise SystemExit(f"no bench.py JSON line in {a.bench_log}")
+        roof = line.get("roofline", {})
+        if a.aes is None:
+            a.aes = int(roof.get("algorithmic_aes_per_launch") or roof.get("algorithmic_aes_per_pass"))
+        if a.bytes is None:
+            a.bytes = int(roof.get("algorithmic_bytes_per_launch") or 0)
+        if a.leaves is None and line.get("config", {}).get("outputs_per_gpu"):
+            a.leaves = int(line["config"]["outputs_per_gpu"])
+        res["bench_launch_ms"] = roof.get("launch_ms") or roof.get("launch_ms_per_pass")
+        res["bench_config"] = line.get("config", {}).get("workload")
+    if a.aes is None or a.bytes is None:
+        raise SystemExit("--aes and --bytes (or --bench-log) are required")
     # Per-launch mode keeps only the launches with the largest grid: a bench
     # run's spot checks call the same kernel on a few points.
     durs = []
@@ -51,8 +84,10 @@ def main():
         if not a.total and a.skip and len(sel) > a.skip:
             skipped, sel = a.skip, sel[a.skip:]
         res.update(kernel=durs[0][2], calls=len(sel), warmup_launches_skipped=skipped,
-                   avg_ns=(sum(sel) if a.total else sum(sel) / len(sel)), min_ns=min(sel),
-                   max_ns=max(sel))
+                   avg_ns=(sum(sel) / a.passes if a.total else sum(sel) / len(sel)),
+                   min_ns=min(sel), max_ns=max(sel))
+        if a.total:
+            res["passes"] = a.passes
     sums, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
@@ -60,7 +95,7 @@ def main():
                 c = row["Counter_Name"]
                 sums[c] += float(row["Counter_Value"])
                 launches[c].add(row["Dispatch_Id"])
-    per = {c: sums[c] / (1 if a.total else len(launches[c])) for c in sums}
+    per = {c: sums[c] / (a.passes if a.total else len(launches[c])) for c in sums}
     res["counters_per_launch"] = per
     aes = a.aes
     res["aes_blocks_per_launch"] = aes
