@@ -37,6 +37,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -152,6 +153,26 @@ def host_cpu(threads: int = None) -> dict:
             "threads_used": threads if threads is not None else CPU_THREADS}
 
 
+def cgroup_cpus():
+    """CPUs the host's cgroup lets this process use (cpu.max quota / period),
+    or None without a quota: the GPU box's share is 16 of its 256 CPUs."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
+def all_cores_sample(work, items, unit: str, budget_s: float = 8.0) -> dict:
+    """The same CPU work on every host CPU the process may run on
+    (sched_getaffinity), as SURVEY.md 8d asks beside the per-GPU share; the
+    cgroup quota that bounds it is reported with it."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    units, dt, done = run_cpu_pool(work, items, threads=n, budget_s=budget_s)
+    return {"value": units / dt, "unit": unit, "threads": n, "cgroup_cpu_quota": cgroup_cpus(),
+            "sample": f"{done} work items, {dt:.1f} s wall on {n} host threads"}
+
+
 def run_cpu_pool(work, items, threads: int = CPU_THREADS, budget_s: float = 15.0):
     """Runs work(item) -> units over `items` on `threads` host threads (the
     oracle's C calls release the GIL), submitting new items only while the
@@ -231,6 +252,7 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64, vt=None):
     leaves1, dt1, done1 = run_cpu_pool(work, range(n_sub), threads=1, budget_s=4.0)
     return {"value": leaves / dt, "unit": "leaves/s", "cores": CPU_THREADS, "kind": "port",
             "single_thread_value": leaves1 / dt1,
+            "all_cores": all_cores_sample(work, range(n_sub), "leaves/s"),
             "single_thread_sample": f"{done1} subtrees of 2^18 outputs, {dt1:.1f} s on 1 thread",
             "host": host_cpu(),
             "sample": f"{done} of the {n_sub} subtrees of 2^18 {vt} outputs of the benchmark "
@@ -240,31 +262,49 @@ def cpu_baseline(key, log_domain: int, chunks: int, bits: int = 64, vt=None):
             "aes_blocks_per_s": done * (tree_aes_per_launch(sub, b) + top) / dt}
 
 
-def profiled_traffic(kernel: str, leaves_per_launch: int = None):
+def _round_key(path: str):
+    """profiles/r14a_full_domain_summary.json -> (14, "a"): summaries sort by round."""
+    m = re.match(r"r(\d+)([a-z]*)", os.path.basename(path))
+    return (int(m.group(1)), m.group(2)) if m else (0, "")
+
+
+def profiled_traffic(kernel: str, leaves_per_launch: int = None, workload: str = None):
     """Per-launch HBM bytes of the dominant kernel from the newest committed
-    rocprofv3 PMC summary whose kernel name contains `kernel` (and, for the
-    full domain, the same outputs per launch): profiles/<round>_summary.json,
-    written by tools/pmc_summary.py from profiles/profile.sh's passes
-    (FETCH_SIZE/WRITE_SIZE with the gfx950 corrections of MI355X_MICROARCH.md)."""
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
+    rocprofv3 PMC summary of this workload: profiles/<round>_<workload>_summary.json,
+    written by tools/profile_workload.sh (tools/pmc_summary.py --workload) from
+    the same bench.py command (FETCH_SIZE/WRITE_SIZE with the gfx950
+    corrections of MI355X_MICROARCH.md).  Summaries without a workload tag
+    (rounds before r14) are matched by kernel name (and outputs per launch)
+    only when no tagged one exists."""
+    tagged, untagged = [], []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json")):
         try:
             s = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if ("hbm_traffic_bytes" in s
-                and kernel.replace("(anonymous namespace)::", "")
-                in s.get("kernel", "").replace("(anonymous namespace)::", "")
-                and (leaves_per_launch is None or s.get("leaves_per_launch") == leaves_per_launch)):
-            best = (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT),
-                    {"valu_lane_ops_per_aes": s.get("valu_lane_ops_per_aes"),
-                     "lds_lane_ops_per_aes": s.get("lds_lane_ops_per_aes"),
-                     "lds_pipe_busy": s.get("lds_pipe_busy"),
-                     "sustained_clock_ghz": s.get("effective_clock_ghz"),
-                     "clk_per_aes_per_cu": s.get("clk_per_aes_per_cu"),
-                     "write_amplification": s.get("write_amplification"),
-                     "profiled_launch_ms": s.get("avg_ns", 0) / 1e6})
-    return best
+        if "hbm_traffic_bytes" not in s:
+            continue
+        if workload is not None and s.get("workload") == workload:
+            tagged.append((_round_key(f), f, s))
+        elif (s.get("workload") is None
+              and kernel.replace("(anonymous namespace)::", "")
+              in s.get("kernel", "").replace("(anonymous namespace)::", "")
+              and (leaves_per_launch is None or s.get("leaves_per_launch") == leaves_per_launch)):
+            untagged.append((_round_key(f), f, s))
+    if not tagged and not untagged:
+        return None
+    _, f, s = max(tagged or untagged, key=lambda c: (c[0], c[1]))
+    return (s["hbm_traffic_bytes"], os.path.relpath(f, ROOT),
+            {"valu_lane_ops_per_aes": s.get("valu_lane_ops_per_aes"),
+             "lds_lane_ops_per_aes": s.get("lds_lane_ops_per_aes"),
+             "lds_pipe_busy": s.get("lds_pipe_busy"),
+             "sustained_clock_ghz": s.get("effective_clock_ghz"),
+             "clk_per_aes_per_cu": s.get("clk_per_aes_per_cu"),
+             "write_amplification": s.get("write_amplification"),
+             "hbm_write_bytes": s.get("hbm_write_bytes"),
+             "hbm_read_bytes": s.get("hbm_read_bytes_corrected"),
+             "profiled_kernel": s.get("kernel"),
+             "profiled_launch_ms": s.get("avg_ns", 0) / 1e6})
 
 
 def host_output_rate(dpf, ctx0, bits: int, reps: int, dev_out, n: int, kernel_ms: float) -> dict:
@@ -297,19 +337,25 @@ def host_output_rate(dpf, ctx0, bits: int, reps: int, dev_out, n: int, kernel_ms
             "note": "PCIe-inclusive; the kernel-level `value` keeps the outputs in HBM"}
 
 
-def profile_check(roof: dict, tr, aes_per_launch: float, ms_per_launch: float) -> None:
+def profile_check(roof: dict, tr, aes_per_launch: float, launch_ms: float) -> None:
     """Puts the committed rocprofv3 summary's timed-launch average beside this
-    run's own launch time: `frac_from_profile` is the roofline fraction the
-    summary alone gives, and `profile_slower_than_step` flags a summary whose
-    kernel is slower than this run's whole step (a profile of another box or
-    tree, not of this kernel as measured here)."""
+    run's own HIP-event launch time: `frac_from_profile` is the roofline
+    fraction the summary alone gives, `profile_vs_launch` their ratio (a
+    summary of this kernel on this tree agrees within a few per cent)."""
     if not tr or not tr[2] or not tr[2].get("profiled_launch_ms"):
         return
     prof_ms = tr[2]["profiled_launch_ms"]
     roof["profiled_launch_ms"] = prof_ms
     roof["frac_from_profile"] = aes_per_launch / (prof_ms * 1e-3) / 1e9 / roof["peak"]
-    roof["profile_vs_launch"] = prof_ms / ms_per_launch
-    roof["profile_slower_than_step"] = bool(prof_ms > ms_per_launch)
+    roof["profile_vs_launch"] = prof_ms / launch_ms
+    roof["profile_within_3pct"] = bool(abs(prof_ms / launch_ms - 1) <= 0.03)
+
+
+def workload_tag(args) -> str:
+    """The tools/profile_workload.sh tag of this bench workload (profiles/<round>_<tag>_summary.json)."""
+    if args.workload == "full_domain_tuple":
+        return f"full_domain_tuple_{args.tuple_type}"
+    return args.workload
 
 
 def kernel_name(args, bits: int) -> str:
@@ -460,8 +506,8 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     if rank == 0:
-        tr = (profiled_traffic(kernel_name(args, bits), outputs_per_rank)
-              if args.workload in ("full_domain", "full_domain_tuple") else None)
+        tr = (profiled_traffic(kernel_name(args, bits), outputs_per_rank, workload=workload_tag(args))
+              if args.log_domain == (31 if bits == 128 else LOG_PER_GPU) else None)
         vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
                  "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "
                                                       "IntModN<uint32_t, 4294967291>>",
@@ -503,7 +549,7 @@ def main():
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS},
         }
-        profile_check(res["roofline"], tr, aes_per_launch, ms_per_step)
+        profile_check(res["roofline"], tr, aes_per_launch, kern_ms_max)
         if args.host_output and world == 1 and args.workload in ("full_domain", "full_domain_u128"):
             res["api_level"] = host_output_rate(dpf, ctx0, bits, args.host_output_reps, out,
                                                 outputs_per_rank, kern_ms_max)
@@ -567,6 +613,7 @@ def cpu_baseline_points(dpf, batch, host_points, keys: int, ppk: int):
     n1, dt1, done1 = run_cpu_pool(work, range((nk + chunk - 1) // chunk), threads=1, budget_s=3.0)
     return {"value": n / dt, "unit": "points/s", "cores": T, "kind": "port", "host": host_cpu(T),
             "single_thread_value": n1 / dt1,
+            "all_cores": all_cores_sample(work, range((nk + chunk - 1) // chunk), "points/s"),
             "published_reference_single_thread": "335K points/s (2^20 points at log 128 in "
                                                  "3.13 s, experiments/README.md:98-107, one "
                                                  "Xeon thread @ 2.3 GHz)",
@@ -703,7 +750,8 @@ def main_evaluate_at(args):
     achieved = aes_per_launch / (kern_ms_max * 1e-3) / 1e9
     kname = ("eval_points_kernel<(anonymous namespace)::GenericLeaf, 64, true, true, %s" %
              ("true>" if summed else "false, true>"))
-    tr = profiled_traffic(kname) if n_keys == 1 << 20 and world == 1 else None
+    tr = (profiled_traffic(kname, workload=args.workload)
+          if n_keys == 1 << 20 and ppk == 1 << 10 and world == 1 else None)
     if rank == 0:
         res = {
             "metric": EA_SUM_METRIC if summed else EA_METRIC,
@@ -726,6 +774,7 @@ def main_evaluate_at(args):
                             launch_ms=kern_ms_max, algorithmic_aes_per_launch=aes_per_launch),
             "process_group": ginfo,
         }
+        profile_check(res["roofline"], tr, aes_per_launch, kern_ms_max)
         if world == 1 and not args.no_cpu_baseline:
             nb = min(nk, 32768)
             if summed:
@@ -887,7 +936,8 @@ def main_heavy_hitters(args):
     aes_rank = HH.algorithmic_aes(dpf, logs, record, hi - lo, walk=not cache) * 2
     aes_total = HH.algorithmic_aes(dpf, logs, record, n_keys, walk=not cache) * 2
     achieved = aes_rank / (kern_ms_max * 1e-3) / 1e9
-    tr = (profiled_traffic("batch_level_kernel<(anonymous namespace)::Mod32V<2, true>, 2, true>")
+    tr = (profiled_traffic("batch_level_kernel<(anonymous namespace)::Mod32V<2, true>, 2, true>",
+                           workload="heavy_hitters")
           if n_keys == 1 << 20 and world == 1 and args.top_k == 1024 else None)
     if rank == 0:
         ref = HH.plaintext_prefix_counts(values, idx, 128)
@@ -914,12 +964,13 @@ def main_heavy_hitters(args):
             "verified": ("two-server reconstruction == plaintext prefix histogram at every level"
                          if verified else False),
             "true_top_k_recall": len(true_top & set(final)) / max(len(true_top), 1),
-            **aes_rooflines(achieved, "batch_level_kernel<Mod32V, 2, true>",
+            **aes_rooflines(achieved, "hh_level_kernel (cached levels) + batch_level_kernel<Mod32V, 2, true> (level 0)",
                             traffic=tr[0] if tr else None, traffic_unit="bytes per pass",
                             traffic_source=tr[1] if tr else None, pmc=tr[2] if tr else None,
                             launch_ms_per_pass=kern_ms_max, algorithmic_aes_per_pass=aes_rank),
             "process_group": ginfo,
         }
+        profile_check(res["roofline"], tr, aes_rank, kern_ms_max)
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_heavy_hitters(logs, record, alphas, seeds,
                                                              args.top_k)
@@ -1010,7 +1061,7 @@ def main_dcf(args):
     aes_per_eval = h2t[-1] + (h2t[-1] + 1)      # walk + one value hash per depth
     aes_launch = nk * ppk * aes_per_eval
     achieved = aes_launch / (kern_ms_max * 1e-3) / 1e9
-    tr = (profiled_traffic("dcf_fast_kernel<64, false, true, 1>")
+    tr = (profiled_traffic("dcf_fast_kernel<64, false, true, 1>", workload="dcf")
           if (n_keys, ppk, n, world) == (1 << 16, 1 << 10, 64, 1) else None)
     if rank == 0:
         res = {
@@ -1030,6 +1081,7 @@ def main_dcf(args):
                             launch_ms=kern_ms_max, algorithmic_aes_per_launch=aes_launch),
             "process_group": ginfo,
         }
+        profile_check(res["roofline"], tr, aes_launch, kern_ms_max)
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O

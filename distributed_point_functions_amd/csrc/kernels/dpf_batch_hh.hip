@@ -33,9 +33,22 @@ using namespace dpf_rt;
 #define DPF_HH_RESIGMA 1
 #endif
 
+// 1: the second leaf pair waits in LDS (32 B per thread beside the 128 KiB of
+// tables) while the first pair is hashed, instead of in 10 VGPRs.
+#ifndef DPF_HH_STASH
+#define DPF_HH_STASH 1
+#endif
+
 namespace {
 
 constexpr int kHHBlock = 256 * DPF_HH_WAVES;
+
+struct HHLds {
+  uint32_t tab[kTabWords];
+#if DPF_HH_STASH
+  uint4 stash[2][kHHBlock];  // [leaf 2 / 3][thread]: seed | control bit
+#endif
+};
 
 struct HHParams {
   int64_t num_keys;
@@ -116,10 +129,14 @@ __device__ __forceinline__ void hash_leaf_pair(const LdsLookup& lk, const uint32
 
 __global__ __launch_bounds__(kHHBlock) __attribute__((amdgpu_waves_per_eu(DPF_HH_WAVES, DPF_HH_WAVES)))
 void hh_level_kernel(HHParams p) {
-  __shared__ LdsImage lds;
+  __shared__ HHLds lds;
   fill_tables(lds.tab);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const uint32_t lt = (threadIdx.x & 31) * 4u;
+  uint32_t m1;
+  asm volatile("v_mov_b32 %0, 0xff00" : "=v"(m1));
+  const LdsLookup lk{reinterpret_cast<const char*>(lds.tab),
+                     {lt, lt + 128u, lt + 65536u, lt + 65664u}, m1};
   const int64_t U = p.num_starts;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.num_threads;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -180,8 +197,22 @@ void hh_level_kernel(HHParams p) {
       const uint32_t corr[2] = {(uint32_t)vc[0].low, p.nl > 1 ? (uint32_t)vc[1].low : 0u};
       const UniformRK rk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
                                UniformRK{p.rkv.k}};
+#if DPF_HH_STASH
+      lds.stash[0][threadIdx.x] = make_uint4(L[2].w0 | tl[2], L[2].w1, L[2].w2, L[2].w3);
+      lds.stash[1][threadIdx.x] = make_uint4(L[3].w0 | tl[3], L[3].w1, L[3].w2, L[3].w3);
+#endif
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
+#if DPF_HH_STASH
+        if (pr == 1) {
+          // Same thread wrote these: no barrier needed.
+          const uint4 a = lds.stash[0][threadIdx.x], c = lds.stash[1][threadIdx.x];
+          tl[2] = a.x & 1u;
+          tl[3] = c.x & 1u;
+          L[2] = Block4{a.x & ~1u, a.y, a.z, a.w};
+          L[3] = Block4{c.x & ~1u, c.y, c.z, c.w};
+        }
+#endif
         Block4 h[4];
         if (p.b == 2) {
           hash_leaf_pair(lk, p.rkv.k, L[2 * pr], L[2 * pr + 1], h);

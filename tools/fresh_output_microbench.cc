@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <malloc.h>
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -71,11 +72,19 @@ int main() {
   char* bounce[2];
   for (auto& b : bounce) CHECK(hipHostMalloc((void**)&b, kChunk, hipHostMallocDefault));
   CHECK(hipDeviceSynchronize());
-  const char* names[] = {"reg", "reg+thp", "bounce", "bounce+thp", "bounce16", "reg_prefault"};
+  const char* names[] = {"reg", "reg+thp", "bounce", "bounce+thp", "bounce16", "reg_prefault",
+                         "bounce+thp+prefault", "bounce+thp, malloc keeps pages"};
   for (size_t mib : {8, 16, 24, 32, 48, 64, 128, 256}) {
     const size_t bytes = mib << 20;
-    for (int var = 0; var < 6; ++var) {
-      const bool reg = var == 0 || var == 1 || var == 5, thp = var == 1 || var == 3;
+    for (int var = 0; var < 8; ++var) {
+      const bool reg = var == 0 || var == 1 || var == 5, thp = var == 1 || var == 3 || var >= 6;
+      // Variant 7: glibc serves large blocks from the heap and keeps freed
+      // pages (no mmap/munmap per call): what the per-call cost is without
+      // the allocator's fresh pages.
+      if (var == 7) {
+        mallopt(M_MMAP_MAX, 0);
+        mallopt(M_TRIM_THRESHOLD, 1 << 30);
+      }
       const int threads = var == 4 ? 16 : 8;
       std::vector<double> tot, t_alloc, t_copy, t_free;
       for (int it = 0; it < 27; ++it) {
@@ -84,7 +93,7 @@ int main() {
         v->reserve(bytes / 8);
         char* d = reinterpret_cast<char*>(v->data());
         if (thp) advise(d, bytes);
-        if (var == 5) {
+        if (var == 5 || var == 6) {
           std::vector<std::thread> t;
           for (int i = 0; i < 16; ++i) {
             const size_t lo = bytes * i / 16, hi = bytes * (i + 1) / 16;
@@ -139,6 +148,10 @@ int main() {
              mib, names[var], med(tot), mx(tot), med(t_alloc), med(t_copy), med(t_free),
              mx(t_copy), mx(t_free));
       fflush(stdout);
+      if (var == 7) {
+        mallopt(M_MMAP_MAX, 65536);
+        mallopt(M_TRIM_THRESHOLD, 128 * 1024);
+      }
     }
   }
   return 0;
