@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <malloc.h>
 #include <functional>
 #include <numeric>
 #include <random>
@@ -426,8 +427,16 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--benchmark_min_time=")) r.min_time = std::atof(v);
     else if (const char* v = val("--json=")) json = v;
     else if (a == "--split") r.split = true;
+    else if (a == "--malloc_keep_pages") {
+      // Harness option, off by default: glibc serves every block from its heap
+      // and keeps freed pages, so a result vector of >= 32 MiB is not a fresh
+      // mmap (page faults, zeroing) plus a munmap per call -- what the
+      // mid-size per-call cost is without the allocator's fresh pages.
+      mallopt(M_MMAP_MAX, 0);
+      mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    }
     else {
-      std::fprintf(stderr, "usage: %s [--benchmark_filter=RE] [--benchmark_min_time=S] [--json=PATH] [--split]\n",
+      std::fprintf(stderr, "usage: %s [--benchmark_filter=RE] [--benchmark_min_time=S] [--json=PATH] [--split] [--malloc_keep_pages]\n",
                    argv[0]);
       return 2;
     }

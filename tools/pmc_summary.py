@@ -27,7 +27,7 @@ CUS = 256
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("kernel")
+    ap.add_argument("kernel", help="kernel name substring; alternatives separated by |")
     ap.add_argument("--aes", type=int, default=None, help="algorithmic AES blocks per launch")
     ap.add_argument("--bytes", type=int, default=None, help="algorithmic bytes written per launch")
     ap.add_argument("--bench-log", default=None,
@@ -73,7 +73,7 @@ def main():
     durs = []
     for f in glob.glob(os.path.join(a.dir, "trace", "*kernel_trace.csv")):
         for row in csv.DictReader(open(f)):
-            if a.kernel in row["Kernel_Name"].replace("(anonymous namespace)::", ""):
+            if any(k in row["Kernel_Name"].replace("(anonymous namespace)::", "") for k in a.kernel.split("|")):
                 durs.append((int(row["Grid_Size_X"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"]),
                              row["Kernel_Name"], int(row["Start_Timestamp"])))
     grid = max(d[0] for d in durs) if durs else None
@@ -91,7 +91,8 @@ def main():
     sums, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            if a.kernel in row["Kernel_Name"].replace("(anonymous namespace)::", "") and (a.total or int(row["Grid_Size"]) == grid):
+            if (any(k in row["Kernel_Name"].replace("(anonymous namespace)::", "") for k in a.kernel.split("|"))
+                    and (a.total or int(row["Grid_Size"]) == grid)):
                 c = row["Counter_Name"]
                 sums[c] += float(row["Counter_Value"])
                 launches[c].add(row["Dispatch_Id"])

@@ -117,6 +117,27 @@ __host__ __device__ inline uint32_t mix32(uint32_t x) {
   return x;
 }
 
+// 32 x 32 bit-matrix transpose of a[0..31] (a[i] bit j <-> a[j] bit i): the
+// conversion between 32 blocks' words and their bit planes that a bitslice
+// wave pays on its inputs (leaf seeds) and outputs (hashes).
+__device__ __forceinline__ void transpose32(uint32_t* a) {
+#pragma unroll
+  for (int j = 16, sh = 0; j != 0; j >>= 1, ++sh) {
+    const uint32_t m = j == 16 ? 0x0000ffffu : j == 8 ? 0x00ff00ffu : j == 4 ? 0x0f0f0f0fu
+                     : j == 2 ? 0x33333333u : 0x55555555u;
+#pragma unroll
+    for (int k = 0; k < 32; k = ((k | j) + 1) & ~j) {
+      const uint32_t t = (a[k] ^ (a[k | j] >> j)) & m;
+      a[k] ^= t;
+      a[k | j] ^= t << j;
+    }
+  }
+}
+
+// TRANSPOSES = 1: every iteration also converts the 128 planes to words and
+// back (4 + 4 transposes; net identity), the layout changes a bitslice wave
+// fed by and feeding ordinary blocks pays.
+template <int TRANSPOSES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void b_kernel(int iters, uint32_t* out) {
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -125,6 +146,12 @@ void b_kernel(int iters, uint32_t* out) {
   for (int p = 0; p < 128; ++p) s[p] = mix32(gid * 128u + p);
   const CKeys ck;
   for (int it = 0; it < iters; ++it) {
+    if (TRANSPOSES) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) transpose32(s + 32 * q);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) transpose32(s + 32 * q);
+    }
     FFRegs ff;
     uint32_t o[128];
     fbs::sigma_ark0(s, ck, ff);
@@ -187,7 +214,7 @@ int main(int argc, char** argv) {
   CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
   CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
   // Bitslice correctness on two lanes.
-  b_kernel<<<cus, 256, 0, s2>>>(2, db);
+  b_kernel<1><<<cus, 256, 0, s2>>>(2, db);
   CK(hipStreamSynchronize(s2));
   {
     std::vector<uint32_t> h((size_t)cus * 256);
@@ -219,9 +246,11 @@ int main(int argc, char** argv) {
     CK(hipEventSynchronize(tm.b));
     return tm.ms();
   };
+  int tr = 0;   // transposes in the bitslice kernel (second pass)
   auto run_b4 = [&](int it) {
     CK(hipEventRecord(tm.a, s2));
-    hipLaunchKernelGGL(b_kernel, dim3(cus), dim3(256), 0, s2, it, db);
+    if (tr) hipLaunchKernelGGL(b_kernel<1>, dim3(cus), dim3(256), 0, s2, it, db);
+    else hipLaunchKernelGGL(b_kernel<0>, dim3(cus), dim3(256), 0, s2, it, db);
     CK(hipEventRecord(tm.b, s2));
     CK(hipEventSynchronize(tm.b));
     return tm.ms();
@@ -233,29 +262,35 @@ int main(int argc, char** argv) {
   const double t4_aes = (double)cus * 256 * t4_iters * kTAesPerIter;   // 4 of 16 waves work
   const float t4 = best([&] { return run_t4(t4_iters); });
   printf("{\"case\": \"T4\", \"ms\": %.3f, \"g_aes_per_s\": %.2f}\n", t4, t4_aes / t4 / 1e6);
-  const float b4 = best([&] { return run_b4(b_iters); });
-  const double b_aes_per_iter = (double)cus * 256 * 32;
-  printf("{\"case\": \"B4\", \"iters\": %d, \"ms\": %.3f, \"g_aes_per_s\": %.2f}\n", b_iters, b4,
-         b_aes_per_iter * b_iters / b4 / 1e6);
-  // Both at once, the bitslice part sized to last as long as T4 alone.
-  const int bi = (int)(b_iters * t4 / b4 + 0.5);
-  Timer t2;
-  float both = 1e30f;
-  for (int rep = 0; rep < 5; ++rep) {
-    CK(hipDeviceSynchronize());
-    CK(hipEventRecord(tm.a, s1));
-    CK(hipStreamWaitEvent(s2, tm.a, 0));
-    hipLaunchKernelGGL(t_kernel, dim3(cus), dim3(1024), 0, s1, k[0], k[1], k[2], t4_iters, dt, 4);
-    hipLaunchKernelGGL(b_kernel, dim3(cus), dim3(256), 0, s2, bi, db);
-    CK(hipEventRecord(t2.b, s2));
-    CK(hipStreamWaitEvent(s1, t2.b, 0));
-    CK(hipEventRecord(tm.b, s1));
-    CK(hipEventSynchronize(tm.b));
-    const float x = tm.ms();
-    if (rep && x < both) both = x;
+  for (tr = 0; tr <= 1; ++tr) {
+    const float b4 = best([&] { return run_b4(b_iters); });
+    const double b_aes_per_iter = (double)cus * 256 * 32;
+    printf("{\"case\": \"B4\", \"transposes\": %d, \"iters\": %d, \"ms\": %.3f, "
+           "\"g_aes_per_s\": %.2f}\n", tr, b_iters, b4, b_aes_per_iter * b_iters / b4 / 1e6);
+    // Both at once, the bitslice share swept around the balance point.
+    for (int pct : {50, 75, 100, 125}) {
+      const int bi = (int)(b_iters * t4 / b4 * pct / 100.0 + 0.5);
+      Timer t2;
+      float both = 1e30f;
+      for (int rep = 0; rep < 5; ++rep) {
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(tm.a, s1));
+        CK(hipStreamWaitEvent(s2, tm.a, 0));
+        hipLaunchKernelGGL(t_kernel, dim3(cus), dim3(1024), 0, s1, k[0], k[1], k[2], t4_iters, dt, 4);
+        if (tr) hipLaunchKernelGGL(b_kernel<1>, dim3(cus), dim3(256), 0, s2, bi, db);
+        else hipLaunchKernelGGL(b_kernel<0>, dim3(cus), dim3(256), 0, s2, bi, db);
+        CK(hipEventRecord(t2.b, s2));
+        CK(hipStreamWaitEvent(s1, t2.b, 0));
+        CK(hipEventRecord(tm.b, s1));
+        CK(hipEventSynchronize(tm.b));
+        const float x = tm.ms();
+        if (rep && x < both) both = x;
+      }
+      const double tot = t4_aes + b_aes_per_iter * bi;
+      printf("{\"case\": \"T4+B4\", \"transposes\": %d, \"b_share\": %.3f, \"b_iters\": %d, "
+             "\"ms\": %.3f, \"g_aes_per_s\": %.2f, \"vs_T16\": %.3f}\n", tr,
+             b_aes_per_iter * bi / tot, bi, both, tot / both / 1e6, tot / both / (t16_aes / t16));
+    }
   }
-  printf("{\"case\": \"T4+B4\", \"b_iters\": %d, \"ms\": %.3f, \"g_aes_per_s\": %.2f, "
-         "\"vs_T16\": %.3f}\n", bi, both, (t4_aes + b_aes_per_iter * bi) / both / 1e6,
-         (t4_aes + b_aes_per_iter * bi) / both / (t16_aes / t16));
   return 0;
 }
