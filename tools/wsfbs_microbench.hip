@@ -122,15 +122,19 @@ __host__ __device__ inline uint32_t mix32(uint32_t x) {
 // wave pays on its inputs (leaf seeds) and outputs (hashes).
 __device__ __forceinline__ void transpose32(uint32_t* a) {
 #pragma unroll
-  for (int j = 16, sh = 0; j != 0; j >>= 1, ++sh) {
-    const uint32_t m = j == 16 ? 0x0000ffffu : j == 8 ? 0x00ff00ffu : j == 4 ? 0x0f0f0f0fu
-                     : j == 2 ? 0x33333333u : 0x55555555u;
+  for (int st = 0; st < 5; ++st) {
+    const int j = 16 >> st;
+    const uint32_t m = st == 0 ? 0x0000ffffu : st == 1 ? 0x00ff00ffu : st == 2 ? 0x0f0f0f0fu
+                     : st == 3 ? 0x33333333u : 0x55555555u;
 #pragma unroll
-    for (int k = 0; k < 32; k = ((k | j) + 1) & ~j) {
-      const uint32_t t = (a[k] ^ (a[k | j] >> j)) & m;
-      a[k] ^= t;
-      a[k | j] ^= t << j;
-    }
+    for (int blk = 0; blk < 32; blk += 2 * j)
+#pragma unroll
+      for (int i = 0; i < j; ++i) {
+        const int k = blk + i;
+        const uint32_t t = (a[k] ^ (a[k + j] >> j)) & m;
+        a[k] ^= t;
+        a[k + j] ^= t << j;
+      }
   }
 }
 
