@@ -958,6 +958,8 @@ def main_heavy_hitters(args):
                        "parallelism": f"key-batch x{world}"},
             "seconds_per_pass": elapsed / args.steps,
             "expansion_cache": cache,
+            "expansion_cache_events": [dict(srv.ctx.cache_events) for srv in servers],
+            "batch_context_device_bytes": [int(srv.ctx.device_bytes) for srv in servers],
             "outputs_per_pass": outputs_per_pass,
             "aes_blocks_per_s": aes_total * args.steps / elapsed,
             "keygen_s_rank0": keygen_s, "keygen_threads": threads,

@@ -63,8 +63,8 @@ bool CacheOn() {
   const char* v = std::getenv("DPF_BATCH_NO_CACHE");
   return !(v && v[0] == '1');
 }
-// DPF_BATCH_CACHE_IN_PLACE=1 acts as if no spare cache buffer fitted (gather
-// the start seeds, rewrite the cache in place): a test hook for that path.
+// DPF_BATCH_CACHE_IN_PLACE=1 acts as if no spare cache buffer fitted (the
+// cache is rewritten in place): a test hook for that path.
 bool SpareOff() {
   const char* v = std::getenv("DPF_BATCH_CACHE_IN_PLACE");
   return v && v[0] == '1';
@@ -141,18 +141,22 @@ Status DeviceBatchContext::Ensure(void** p, size_t* cap, size_t bytes) {
 }
 
 void DeviceBatchContext::ReleaseExpansionCache() {
+  // hipFree waits for the device work that may still read the buffers.
   Release(&leaf_seeds_, &leaf_seeds_cap_);
   Release(&leaf_spare_, &leaf_spare_cap_);
   Release(&slots_, &slots_cap_);
   leaf_level_ = -1;
 }
 
-void DeviceBatchContext::Reset() {
+void DeviceBatchContext::Reset(bool release_expansion_cache) {
   previous_hierarchy_level_ = -1;
   partial_evaluations_level_ = -1;
   partial_prefixes_.clear();
-  (void)dpf_hip_stream_sync(nullptr);  // work still reading the cache
-  ReleaseExpansionCache();
+  leaf_level_ = -1;
+  if (release_expansion_cache) {
+    (void)dpf_hip_stream_sync(nullptr);  // work still reading the cache
+    ReleaseExpansionCache();
+  }
 }
 
 DeviceBatchContext::~DeviceBatchContext() {
@@ -565,12 +569,13 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   ctx.leaf_level_ = leaf_seeds ? hierarchy_level : -1;
   ctx.leaf_de_ = dE;
   ctx.leaf_stride_ = leaf_stride;
-  if (hierarchy_level == H - 1 && (ctx.leaf_seeds_ || ctx.leaf_spare_)) {
-    // Nothing reads the cache after the last level: give its memory back
-    // once this call's kernel has read it.
-    HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
-    ctx.ReleaseExpansionCache();
-  }
+  // After the last level nothing reads the cache; its buffers stay allocated
+  // for the next pass over the hierarchy (Reset()), because giving them back
+  // and regrowing them level by level (4, 16, 64 GiB for 2^20 heavy-hitters
+  // clients) cost 3.7 s per 22 s pass (profiles/r14_ab.txt).  The 1/8-of-HBM
+  // headroom rule above bounds what they take; callers that need the memory
+  // call ReleaseExpansionCache() (or Reset(true)).
+  if (hierarchy_level == H - 1) ctx.leaf_level_ = -1;
   if (g_timing_on) dpf_hip_stream_sync(stream);  // attribute device time to its phase
   clk.mark(4);
   // Context update (cc:435-451, 494-496).

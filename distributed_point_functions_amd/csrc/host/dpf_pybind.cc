@@ -472,7 +472,9 @@ PYBIND11_MODULE(_dpf_host, m) {
       .def("fail_next_allocations_for_testing",
            [](PyBatchContext& c, int n, int skip) { c.ctx->FailNextAllocationsForTesting(n, skip); },
            py::arg("n"), py::arg("skip") = 0)
-      .def("reset", [](PyBatchContext& c) { c.ctx->Reset(); });
+      .def("reset", [](PyBatchContext& c, bool release) { c.ctx->Reset(release); },
+           py::arg("release_expansion_cache") = false)
+      .def("release_expansion_cache", [](PyBatchContext& c) { c.ctx->ReleaseExpansionCache(); });
   py::class_<PyKeyBatch>(m, "KeyBatch")
       .def_property_readonly("num_keys", &PyKeyBatch::NumKeys)
       .def_property_readonly("num_levels", &PyKeyBatch::NumLevels)

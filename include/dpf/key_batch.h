@@ -104,9 +104,13 @@ class DeviceBatchContext {
   const dpf_block* partial_seeds() const { return static_cast<const dpf_block*>(seeds_); }
   const uint8_t* partial_control() const { return static_cast<const uint8_t*>(ctrl_); }
   // Back to the state CreateBatchEvaluationContext returns, keeping the
-  // per-call device allocations for the next pass over the hierarchy; the
-  // expansion cache (up to K x 4096 x 16 B) is released.
-  void Reset();
+  // device allocations for the next pass over the hierarchy; with
+  // `release_expansion_cache` the expansion cache (up to K x 4096 x 16 B per
+  // buffer) is given back too.
+  void Reset(bool release_expansion_cache = false);
+  // Frees the expansion cache's buffers (the next call walks down from the
+  // partial evaluations and rebuilds it).  Outputs are unaffected.
+  void ReleaseExpansionCache();
   // Hierarchy level whose call wrote the expansion cache (-1: none).
   int expansion_cache_level() const { return leaf_level_; }
   // Device bytes this context holds (partial evaluations, expansion cache,
@@ -116,7 +120,7 @@ class DeviceBatchContext {
   struct CacheEvents {
     int64_t cache_refused = 0;   // no room for the cache: the call wrote none
     int64_t spare_refused = 0;   // no room for a spare: start seeds gathered, cache rewritten in place
-    int64_t in_place = 0;        // calls that took the gather + in-place path
+    int64_t in_place = 0;        // calls that gathered their start seeds, then rewrote the cache
     int64_t evicted_spare = 0;   // spare freed so a per-call buffer fits
     int64_t evicted_cache = 0;   // unread cache freed so a per-call buffer fits
     int64_t alloc_failures = 0;  // per-call allocations that failed (before any eviction)
@@ -141,7 +145,6 @@ class DeviceBatchContext {
   // Free and total device memory as this context sees it (DPF_BATCH_ALLOC_LIMIT
   // replaces the device's figures with the limit, as a test hook).
   void MemInfo(size_t* free_bytes, size_t* total_bytes) const;
-  void ReleaseExpansionCache();
 
   const DeviceKeyBatch* keys_;
   int previous_hierarchy_level_ = -1;

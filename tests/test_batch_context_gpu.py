@@ -284,9 +284,12 @@ def test_cache_spare_evicted_for_per_call_buffer(sum_mode):
     ev = bctx.cache_events
     assert failed == [] and ev["evicted_spare"] == 1 and ev["evicted_cache"] == 0, ev
     assert ev["alloc_failures"] == 1, ev
-    # After the last level the cache is released: nothing but per-call state.
+    # After the last level nothing reads the cache; an explicit release gives
+    # its memory back.
     assert bctx.expansion_cache_level == -1
-    assert held[-1] < max(held)
+    before = bctx.device_bytes
+    bctx.release_expansion_cache()
+    assert bctx.device_bytes < before
 
 
 @pytest.mark.parametrize("sum_mode", [False, True])
@@ -351,7 +354,8 @@ def test_allocation_limit_too_small_is_resource_exhausted(monkeypatch):
 
 
 def test_reset_releases_expansion_cache():
-    """Reset() gives the expansion cache's memory back."""
+    """Reset(release_expansion_cache=True) gives the expansion cache's memory
+    back; plain Reset() keeps it for the next pass."""
     import torch
     levels, plan = HH5
     dpf, P, rng, batch, oks, _, _, _ = _setup(levels, 40, seed=96)
@@ -363,6 +367,12 @@ def test_reset_releases_expansion_cache():
     assert bctx.expansion_cache_level == 1
     before = bctx.device_bytes
     bctx.reset()
+    assert bctx.expansion_cache_level == -1 and bctx.device_bytes == before
+    dpf.evaluate_until_batch_to_device(0, [], bctx, out)
+    dpf.evaluate_until_batch_to_device(1, [0, 1, 5], bctx, out)
+    torch.cuda.synchronize()
+    assert bctx.expansion_cache_level == 1
+    bctx.reset(release_expansion_cache=True)
     assert bctx.expansion_cache_level == -1 and bctx.device_bytes < before
     dpf.evaluate_until_batch_to_device(0, [], bctx, out)
     assert bctx.expansion_cache_level == 0

@@ -32,6 +32,7 @@ part1)
   timeout -k 10 300 distributed_point_functions_amd/lib/dpf_benchmark --malloc_keep_pages "--benchmark_filter=^BM_EvaluateRegularDpf" > $O/${TAG}_reference_benchmarks_keep_pages.txt 2>&1 || exit 1
   ;;
 part2)
+  [ -s $O/${TAG}_reference_benchmarks_keep_pages.txt ] || timeout -k 10 300 distributed_point_functions_amd/lib/dpf_benchmark --malloc_keep_pages "--benchmark_filter=^BM_EvaluateRegularDpf" > $O/${TAG}_reference_benchmarks_keep_pages.txt 2>&1 || exit 1
   bash tools/bench_all.sh $TAG || exit 1
   ;;
 part3)
