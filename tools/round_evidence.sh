@@ -42,10 +42,12 @@ part3)
   prof $TAG full_domain_tuple_u32x2 "expand_octet_kernel<FastIntLeaf<32, false> >" launch:2 -- --workload full_domain_tuple --tuple-type u32x2 --steps 10 --warmup 2 --no-cpu-baseline
   ;;
 part4)
+  timeout -k 10 400 python bench.py --workload heavy_hitters > $O/bench_${TAG}_heavy_hitters.log 2>&1 || { tail $O/bench_${TAG}_heavy_hitters.log; exit 1; }
+  grep '^{' $O/bench_${TAG}_heavy_hitters.log > $O/bench_${TAG}_heavy_hitters.json
   prof $TAG evaluate_at "eval_points_kernel" launch:1 -- --workload evaluate_at --steps 3 --warmup 1 --no-cpu-baseline
   prof $TAG evaluate_at_sum "eval_points_kernel" launch:1 -- --workload evaluate_at_sum --steps 3 --warmup 1 --no-cpu-baseline
   prof $TAG dcf "dcf_fast_kernel" launch:2 -- --workload dcf --steps 10 --warmup 2 --no-cpu-baseline
-  PROFILE_PASS_LIMIT=400 prof $TAG heavy_hitters "hh_level_kernel|batch_level_kernel<Mod32V<2, true>, 2, true>" total:2 -- --workload heavy_hitters --no-cpu-baseline
+  PROFILE_PASS_LIMIT=400 prof $TAG heavy_hitters "hh_level_kernel|batch_level_kernel<Mod32V<2, true>, 2, true>|gather_seeds_kernel|finalize_sums_kernel" total:2 -- --workload heavy_hitters --no-cpu-baseline
   ;;
 esac
 echo "$PART ok"
