@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <map>
 #include <mutex>
 #include <type_traits>
@@ -929,6 +930,128 @@ int registered_copy(char* h, char* d, size_t bytes, bool to_host, void (*before)
   return rc;
 }
 
+// Maps the pages of fresh host storage [p, p + bytes) by touching one byte per
+// 4 KiB page on up to `threads` threads (a one-thread first touch of a fresh
+// 8 GiB vector costs ~350 ms of page faults, tools/host_output_microbench.cc;
+// registering unmapped pages would fault them in on one thread too).
+void prefault(char* p, size_t bytes, int threads) {
+  constexpr size_t kPage = 4096;
+  const size_t pages = bytes / kPage + 1;
+  size_t t = bytes >> 25;   // one thread per 32 MiB
+  if (t > static_cast<size_t>(threads)) t = threads;
+  auto touch = [p, bytes](size_t lo, size_t hi) {
+    volatile char* v = p;
+    for (size_t i = lo; i < hi; ++i)
+      if (i * kPage < bytes) v[i * kPage] = 0;
+  };
+  if (t <= 1) {
+    touch(0, pages);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (size_t i = 0; i < t; ++i) pool.emplace_back(touch, pages * i / t, pages * (i + 1) / t);
+  for (auto& th : pool) th.join();
+}
+
+// DPF_HIP_D2H_PIPELINE=0 (read per call): a fresh destination of >=
+// kRegisterMin is mapped and registered whole before the first DMA (the r13
+// path), instead of piece by piece behind the DMA.  An A/B hook.
+bool d2h_pipeline_on() {
+  const char* v = std::getenv("DPF_HIP_D2H_PIPELINE");
+  return !(v && v[0] == '0');
+}
+// DPF_HIP_D2H_REGISTER_PIECES=<n> (read per call): the pipelined copy acts as
+// if the registration of its piece n (and every later one) were refused -- a
+// test hook for the bounce fallback of the rest of the range.
+long register_pieces_limit() {
+  const char* v = std::getenv("DPF_HIP_D2H_REGISTER_PIECES");
+  return v && *v ? std::strtol(v, nullptr, 10) : -1;
+}
+
+// A fresh pageable destination of >= kRegisterMin (no registration of ours
+// overlaps it): a helper thread maps (prefault, 8 threads) and registers it in
+// 256 MiB pieces while this thread initialises (before) and DMAs the pieces
+// already registered, so the ~45 ms of mapping and registering 8 GiB runs
+// under the DMA instead of ahead of it.  Piece boundaries are 2 MiB-aligned
+// (no page in two registrations) and every DMA chunk lies in one piece.  A
+// piece whose registration is refused, and everything after it, goes through
+// the bounce buffers.
+constexpr size_t kPiece = size_t{256} << 20;
+
+int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, size_t), void* ctx,
+                  hipStream_t s) {
+  const uintptr_t h0 = reinterpret_cast<uintptr_t>(h), h1 = h0 + bytes;
+  std::vector<uintptr_t> cut{h0};   // piece i = [cut[i], cut[i + 1])
+  for (uintptr_t c = (h0 + kPiece) & ~((uintptr_t{2} << 20) - 1); c < h1; c += kPiece)
+    if (c > cut.back()) cut.push_back(c);
+  cut.push_back(h1);
+  const size_t n = cut.size() - 1;
+  std::vector<int> state(n, 0);   // 0 pending, 1 registered (in g_regs), -1 refused
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<bool> stop{false};
+  int device = 0;
+  (void)hipGetDevice(&device);
+  const long limit = register_pieces_limit();
+  std::thread worker([&] {
+    (void)hipSetDevice(device);
+    for (size_t i = 0; i < n && !stop.load(); ++i) {
+      char* p = reinterpret_cast<char*>(cut[i]);
+      const size_t len = cut[i + 1] - cut[i];
+      prefault(p, len, 8);
+      int st = -1;
+      if (limit >= 0 && static_cast<long>(i) >= limit) {
+        // test hook: refused
+      } else if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+        std::lock_guard<std::mutex> lock(g_reg_mu);
+        g_regs[cut[i]] = Registration{len, 1};
+        g_reg_count.store(static_cast<int>(g_regs.size()));
+        st = 1;
+      } else {
+        (void)hipGetLastError();
+      }
+      {
+        std::lock_guard<std::mutex> lock(mu);
+        state[i] = st;
+      }
+      cv.notify_all();
+      if (st < 0) break;
+    }
+  });
+  int rc = kOk;
+  size_t i = 0;
+  for (; i < n && rc == kOk; ++i) {
+    int st;
+    {
+      std::unique_lock<std::mutex> lock(mu);
+      cv.wait(lock, [&] { return state[i] != 0; });
+      st = state[i];
+    }
+    if (st < 0) break;
+    for (uintptr_t off = cut[i]; off < cut[i + 1] && rc == kOk; off += kStagedChunk) {
+      const size_t len = cut[i + 1] - off < kStagedChunk ? cut[i + 1] - off : kStagedChunk;
+      if (before) before(ctx, off + len - h0);
+      const hipError_t e = hipMemcpyAsync(reinterpret_cast<char*>(off), d + (off - h0), len,
+                                          hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync (registered host memory)");
+    }
+  }
+  stop.store(true);
+  worker.join();
+  if (rc == kOk && i < n) {
+    // Registration refused from piece i on: the rest through the bounce buffers.
+    const size_t off = cut[i] - h0;
+    prefault(h + off, bytes - off, 8);
+    if (before) before(ctx, bytes);
+    rc = bounce_d2h(h + off, d + off, bytes - off, s);
+  }
+  const hipError_t e = hipStreamSynchronize(s);
+  if (rc == kOk && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+  for (size_t j = 0; j < n; ++j)
+    if (state[j] > 0) release_host(cut[j]);
+  return rc;
+}
+
 int bounce_h2d(void* dst, const void* src, size_t bytes, void* stream) {
   std::lock_guard<std::mutex> lock(g_bounce_mu);
   if (int rc = bounce_buffers()) return rc;
@@ -1022,9 +1145,24 @@ int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
                               void* stream) {
   if (!before_chunk) return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
   uintptr_t base = 0;
-  if (bytes >= kRegisterMin && acquire_host(dst, bytes, page_locked(dst), &base) == kAcquired)
-    return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, before_chunk,
-                           ctx, (hipStream_t)stream, base);
+  if (bytes >= kRegisterMin) {
+    const bool locked = page_locked(dst);
+    // An existing registration of ours that contains the range is shared;
+    // a fresh pageable range is mapped and registered piece by piece.
+    const Acquire a = acquire_host(dst, bytes, true, &base);
+    if (a == kAcquired)
+      return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, before_chunk,
+                             ctx, (hipStream_t)stream, base);
+    if (a == kNotOurs && !locked) {
+      if (d2h_pipeline_on())
+        return pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx,
+                             (hipStream_t)stream);
+      prefault((char*)dst, bytes, 16);
+      if (acquire_host(dst, bytes, false, &base) == kAcquired)
+        return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true,
+                               before_chunk, ctx, (hipStream_t)stream, base);
+    }
+  }
   before_chunk(ctx, bytes);
   return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
 }

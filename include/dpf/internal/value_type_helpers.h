@@ -264,13 +264,18 @@ void AdviseHugePages(void* p, size_t bytes);
 void PrefaultPages(void* p, size_t bytes);
 
 // Storage of a fresh std::vector<T> of n elements, reserved, advised onto huge
-// pages and pre-faulted, but still empty (size 0).
+// pages and (with `prefault`) pre-faulted, but still empty (size 0).  The
+// HostSinks below do not pre-fault: their copies map the pages as the data
+// lands (dpf_hip_memcpy_d2h_staged maps and registers a large range piece by
+// piece behind its DMA; below DPF_HIP_REGISTER_MIN_BYTES a 16-thread
+// pre-fault measured slower than faulting chunk by chunk,
+// profiles/r14b_fresh_output_microbench.jsonl).
 template <typename T>
-void ReserveOutputVector(std::vector<T>& out, int64_t n) {
+void ReserveOutputVector(std::vector<T>& out, int64_t n, bool prefault = true) {
   out.clear();
   out.reserve(n);
   AdviseHugePages(out.data(), static_cast<size_t>(n) * sizeof(T));
-  PrefaultPages(out.data(), static_cast<size_t>(n) * sizeof(T));
+  if (prefault) PrefaultPages(out.data(), static_cast<size_t>(n) * sizeof(T));
 }
 
 // A value-initialised std::vector<T> of n elements whose storage was advised
@@ -309,7 +314,7 @@ template <typename T>
 HostSink VectorSink(std::vector<T>* out) {
   HostSink s;
   s.reserve = [out](size_t bytes) -> void* {
-    ReserveOutputVector(*out, static_cast<int64_t>(bytes / sizeof(T)));
+    ReserveOutputVector(*out, static_cast<int64_t>(bytes / sizeof(T)), false);
     return out->data();
   };
   s.grow = [out](size_t bytes) { out->resize((bytes + sizeof(T) - 1) / sizeof(T)); };
@@ -353,7 +358,7 @@ template <typename T>
 HostSink UnpackSink(const std::vector<FlatValueType>* flats, int h, std::vector<T>* out) {
   HostSink s;
   s.reserve = [flats, h, out](size_t bytes) -> void* {
-    ReserveOutputVector(*out, static_cast<int64_t>(bytes / (*flats)[h].packed_size));
+    ReserveOutputVector(*out, static_cast<int64_t>(bytes / (*flats)[h].packed_size), false);
     return nullptr;
   };
   s.chunk = [flats, h, out](const uint8_t* src, size_t offset, size_t len) {

@@ -97,8 +97,10 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
  * chunk's DMA, `before_chunk(ctx, bytes_ready)` is called and must make
  * [0, bytes_ready) of `dst` valid; the DMA of one chunk overlaps the
  * initialisation of the next.  Large copies DMA straight into `dst`
- * (registered for the copy), others go through page-locked staging.  The
- * drop-in EvaluateUntil<T> returns its std::vector<T> this way. */
+ * (registered for the copy; a fresh pageable range is mapped and registered
+ * piece by piece on a helper thread while the DMA fills the pieces already
+ * registered), others go through page-locked staging.  The drop-in
+ * EvaluateUntil<T> returns its std::vector<T> this way. */
 /* Host ranges of at least this many bytes are registered (page-locked) for a
  * copy and DMAed straight into; smaller ones go through page-locked staging. */
 #define DPF_HIP_REGISTER_MIN_BYTES ((size_t)512 << 20)

@@ -366,9 +366,9 @@ def test_evaluate_shard_to_device_errors():
                                     (24, ("tuple", [("int", 32), ("int", 64)]))], ids=str)
 def test_large_host_output_matches_device(log, vt):
     """Host outputs of >= 512 MiB (DPF_HIP_REGISTER_MIN_BYTES) take
-    dpf_hip_memcpy_d2h_staged: the fresh vector is registered and
-    value-initialised chunk by chunk while the previous 64 MiB chunk's DMA
-    runs; smaller ones arrive through the 16 MiB page-locked staging buffers
+    dpf_hip_memcpy_d2h_staged: the fresh vector is mapped and registered piece
+    by piece and value-initialised chunk by chunk while the previous 64 MiB
+    chunk's DMA runs; smaller ones arrive through the 16 MiB page-locked staging buffers
     chunk by chunk (dpf_hip_memcpy_d2h_chunked).  Every byte equals the device
     output, and the two parties' host outputs reconstruct the point function."""
     import torch
@@ -386,6 +386,47 @@ def test_large_host_output_matches_device(log, vt):
     total = O.add_packed(vt, host0.reshape(1 << log, -1), host1.reshape(1 << log, -1))
     nz = np.flatnonzero(total.reshape(1 << log, -1).any(axis=1))
     assert nz.tolist() == [alpha]
+
+
+@pytest.mark.parametrize("env", [{}, {"DPF_HIP_D2H_REGISTER_PIECES": "1"},
+                                 {"DPF_HIP_D2H_REGISTER_PIECES": "0"},
+                                 {"DPF_HIP_D2H_PIPELINE": "0"}], ids=str)
+def test_pipelined_host_output_and_its_fallbacks(env, monkeypatch):
+    """A fresh host output of >= 512 MiB is mapped and registered in 256 MiB
+    pieces by a helper thread while the DMA fills the pieces already
+    registered (dpf_kernels.hip: pipelined_d2h).  A 1 GiB output (five pieces:
+    the vector starts off a 2 MiB boundary) equals the device output byte for
+    byte by default, when the registration of piece 1 or 0 and every later one
+    is refused (the rest of the range through the bounce buffers), and with
+    the pipeline off (map and register the whole range first).  The hooks are
+    read per call."""
+    import torch
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    log = 27
+    dpf = E.params([(log, ("int", 64), 0)])
+    k0, _ = E.generate_keys(dpf, (1 << log) - 777, [[5]], (31, 32))
+    host = dpf.evaluate_until(0, [], dpf.create_evaluation_context(k0), packed=True)
+    dev = torch.empty(host.size, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_until_to_device(0, [], dpf.create_evaluation_context(k0), dev)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(dev.cpu().numpy().reshape(host.shape), host)
+
+
+def test_concurrent_pipelined_host_outputs():
+    """Two threads evaluate 512 MiB host outputs at once (two pipelined
+    copies, each with its own helper thread and registrations): each equals
+    the same key's sequential result."""
+    from concurrent.futures import ThreadPoolExecutor
+    dpf = E.params([(26, ("int", 64), 0)])
+    keys = [E.generate_keys(dpf, 999 + 5 * i, [[i + 2]], (50 + i, 60 + i))[i % 2] for i in range(2)]
+    want = [dpf.evaluate_until(0, [], dpf.create_evaluation_context(k), packed=True) for k in keys]
+    with ThreadPoolExecutor(2) as ex:
+        got = list(ex.map(lambda k: dpf.evaluate_until(0, [], dpf.create_evaluation_context(k),
+                                                         packed=True), keys))
+    for i, g in enumerate(got):
+        np.testing.assert_array_equal(g, want[i])
+    del got, want
 
 
 def test_concurrent_large_host_outputs():

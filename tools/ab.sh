@@ -3,7 +3,7 @@
 # r13_*.sh scripts).  Runs the named pytest files first (parity of what is
 # being compared), then `bench.py <args>` once per variant and round, variants
 # alternating so box drift hits all of them alike, and prints one line per run:
-#   <variant> value unit launch_ms roofline.frac [seconds_per_pass]
+#   <variant> value unit launch_ms roofline.frac [seconds_per_pass] [api_ms per call]
 # A variant is
 #   lib:<name>        vlib/<name>.so copied over the in-tree libdpf_hip.so
 #                     (built by tools/build_variant.sh), restored afterwards;
@@ -51,8 +51,10 @@ for r in $(seq 1 $ROUNDS); do
 import json, sys
 d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 r = d.get("roofline", {})
+api = d.get("api_level", {})
 print(sys.argv[1], f"{d['value']:.4g}", d["unit"], r.get("launch_ms") or r.get("launch_ms_per_pass"),
-      f"{r.get('frac', 0):.4f}", d.get("seconds_per_pass", ""))
+      f"{r.get('frac', 0):.4f}", d.get("seconds_per_pass", ""),
+      f"api_ms {api['api_ms_per_call']}" if api else "")
 PY
   done
 done
