@@ -503,6 +503,18 @@ struct UntilClock {
 };
 }  // namespace
 
+namespace {
+// The split first-call expansion (EvaluateUntilCore): 2^kSplitLevels subtree
+// launches.  DPF_EVAL_SPLIT=0 (read per call) launches the whole tree at
+// once: an A/B hook.
+constexpr int kSplitLevels = 3;
+constexpr int kSplitParts = 1 << kSplitLevels;
+bool SplitOn() {
+  const char* v = std::getenv("DPF_EVAL_SPLIT");
+  return !(v && v[0] == '0');
+}
+}  // namespace
+
 Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<const uint128> prefixes,
                                                    EvaluationContext& ctx,
                                                    const ValueType* requested_type,
@@ -615,6 +627,28 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
   const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());
   const PackedCws o_cw = AddCorrectionWords(ctx.key(), start_level, stop_level, up);
+  // A first call's output of >= DPF_HIP_REGISTER_MIN_BYTES bound for a fresh
+  // host vector: the expansion runs as kSplitParts subtree launches, each
+  // followed by an event, and the copy of part j (dpf_hip_memcpy_d2h_staged_after)
+  // overlaps the expansion of the later parts (2^30 uint64: the 17 ms kernel
+  // no longer precedes the 150 ms DMA).
+  const bool split = host_out && host_out->grow && tree_indices.empty() && SplitOn() &&
+                     L >= kSplitLevels + 12 &&
+                     static_cast<size_t>(total) * esz >= DPF_HIP_REGISTER_MIN_BYTES;
+  size_t o_sub_seed = 0, o_sub_ctrl = 0, o_sub_path = 0;
+  PackedCws o_top{}, o_sub{};
+  if (split) {
+    const dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+    const uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
+    std::vector<dpf_block> roots(kSplitParts, root), paths(kSplitParts);
+    std::vector<uint8_t> parties(kSplitParts, party);
+    for (int j = 0; j < kSplitParts; ++j) paths[j] = ToBlock(static_cast<uint128>(j));
+    o_sub_seed = up.Add(roots.data(), roots.size());
+    o_sub_ctrl = up.Add(parties.data(), parties.size());
+    o_sub_path = up.Add(paths.data(), paths.size());
+    o_top = AddCorrectionWords(ctx.key(), 0, kSplitLevels, up);
+    o_sub = AddCorrectionWords(ctx.key(), kSplitLevels, stop_level, up);
+  }
   clk.mark(6);
   DPF_RETURN_IF_ERROR(up.Commit(stream));
   if (tree_indices.empty()) {
@@ -643,10 +677,32 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   clk.mark(1);
-  HIP_RETURN_IF_ERROR(dpf_hip_expand(start.n, start.seeds, start.ctrl, L, up.Ptr<dpf_block>(o_cw.seed),
-                                     up.Ptr<uint8_t>(o_cw.left), up.Ptr<uint8_t>(o_cw.right), &kl, &kr,
-                                     &kv, &desc, cepb, up.Ptr<dpf_block>(o_vcw),
-                                     ctx.key().party() & 1, expand_out, stream));
+  dpf_internal::PartEvents parts;
+  if (split) {
+    // The subtree roots at depth kSplitLevels (EvaluateSeeds, in place), then
+    // one expansion per subtree into its slice of the output.
+    dpf_block* sub_seed = up.Ptr<dpf_block>(o_sub_seed);
+    uint8_t* sub_ctrl = up.Ptr<uint8_t>(o_sub_ctrl);
+    HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(kSplitParts, kSplitLevels, sub_seed, sub_ctrl,
+                                           up.Ptr<dpf_block>(o_sub_path), up.Ptr<dpf_block>(o_top.seed),
+                                           up.Ptr<uint8_t>(o_top.left), up.Ptr<uint8_t>(o_top.right),
+                                           &kl, &kr, sub_seed, sub_ctrl, stream));
+    const size_t part_bytes = static_cast<size_t>(corrected / kSplitParts) * esz;
+    for (int j = 0; j < kSplitParts; ++j) {
+      HIP_RETURN_IF_ERROR(dpf_hip_expand(
+          1, sub_seed + j, sub_ctrl + j, L - kSplitLevels, up.Ptr<dpf_block>(o_sub.seed),
+          up.Ptr<uint8_t>(o_sub.left), up.Ptr<uint8_t>(o_sub.right), &kl, &kr, &kv, &desc, cepb,
+          up.Ptr<dpf_block>(o_vcw), ctx.key().party() & 1,
+          static_cast<char*>(expand_out) + j * part_bytes, stream));
+      DPF_RETURN_IF_ERROR(parts.Record(part_bytes * (j + 1), stream));
+    }
+  } else {
+    HIP_RETURN_IF_ERROR(dpf_hip_expand(start.n, start.seeds, start.ctrl, L,
+                                       up.Ptr<dpf_block>(o_cw.seed), up.Ptr<uint8_t>(o_cw.left),
+                                       up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, cepb,
+                                       up.Ptr<dpf_block>(o_vcw), ctx.key().party() & 1, expand_out,
+                                       stream));
+  }
   DPF_RETURN_IF_ERROR(up.MarkUsed(stream));
   void* result = expand_out;
   if (!identity) {
@@ -670,7 +726,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     const size_t bytes = static_cast<size_t>(total) * esz;
     void* dst = host_out->reserve(bytes);
     clk.mark(3);
-    HIP_RETURN_IF_ERROR(CopyToHostSink(*host_out, dst, result, bytes, stream));
+    HIP_RETURN_IF_ERROR(CopyToHostSink(*host_out, dst, result, bytes, stream, &parts));
     clk.mark(4);
   }
   return OkStatus();

@@ -36,11 +36,42 @@ inline Status FromHip(int code) {
 }
 #define HIP_RETURN_IF_ERROR(expr) DPF_RETURN_IF_ERROR(::distributed_point_functions::dpf_internal::FromHip(expr))
 
+// Events marking how much of a device output produced in parts on one stream
+// is complete: part j = [0, ends[j]) once events[j] has completed.
+class PartEvents {
+ public:
+  PartEvents() = default;
+  PartEvents(const PartEvents&) = delete;
+  PartEvents& operator=(const PartEvents&) = delete;
+  ~PartEvents() {
+    for (void* e : events_) {
+      (void)dpf_hip_event_sync(e);
+      dpf_hip_event_destroy(e);
+    }
+  }
+  Status Record(size_t end, void* stream) {
+    void* e = nullptr;
+    HIP_RETURN_IF_ERROR(dpf_hip_event_create(&e));
+    events_.push_back(e);
+    ends_.push_back(end);
+    return FromHip(dpf_hip_event_record(e, stream));
+  }
+  int size() const { return static_cast<int>(events_.size()); }
+  void* const* events() const { return events_.data(); }
+  const size_t* ends() const { return ends_.data(); }
+
+ private:
+  std::vector<void*> events_;
+  std::vector<size_t> ends_;
+};
+
 // Copies `bytes` of device output into the storage `dst` a HostSink reserved,
 // letting its grow() initialise each chunk right before that chunk's DMA
-// (dpf_hip_memcpy_d2h_staged).  Returns a dpf_hip status code.
+// (dpf_hip_memcpy_d2h_staged; with `parts`, each chunk's DMA waits only for
+// the part that covers it, dpf_hip_memcpy_d2h_staged_after).  Returns a
+// dpf_hip status code.
 inline int CopyToHostSink(const HostSink& sink, void* dst, const void* src, size_t bytes,
-                          void* stream) {
+                          void* stream, const PartEvents* parts = nullptr) {
   if (sink.chunk && (!dst || bytes < DPF_HIP_REGISTER_MIN_BYTES)) {
     auto consume = [](void* ctx, const void* chunk, size_t offset, size_t len) {
       (*static_cast<const HostSink*>(ctx)).chunk(static_cast<const uint8_t*>(chunk), offset, len);
@@ -52,6 +83,10 @@ inline int CopyToHostSink(const HostSink& sink, void* dst, const void* src, size
   auto before = [](void* ctx, size_t ready) {
     (*static_cast<const std::function<void(size_t)>*>(ctx))(ready);
   };
+  if (parts && parts->size() > 0)
+    return dpf_hip_memcpy_d2h_staged_after(
+        dst, src, bytes, before, const_cast<std::function<void(size_t)>*>(&sink.grow),
+        parts->size(), parts->events(), parts->ends(), stream);
   return dpf_hip_memcpy_d2h_staged(dst, src, bytes, before,
                                    const_cast<std::function<void(size_t)>*>(&sink.grow), stream);
 }

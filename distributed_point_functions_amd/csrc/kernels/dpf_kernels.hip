@@ -978,8 +978,14 @@ long register_pieces_limit() {
 // the bounce buffers.
 constexpr size_t kPiece = size_t{256} << 20;
 
+// With parts (nparts > 0) the DMAs run on `s` = a copy stream of their own:
+// [0, ends[j]) of `d` is ready once events[j] (recorded on the producing
+// stream) has completed, and each chunk's DMA waits on the device for the
+// first part that covers it, so the copy of part j overlaps the work that
+// produces the later parts.
 int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, size_t), void* ctx,
-                  hipStream_t s) {
+                  hipStream_t s, int nparts = 0, void* const* events = nullptr,
+                  const size_t* ends = nullptr) {
   const uintptr_t h0 = reinterpret_cast<uintptr_t>(h), h1 = h0 + bytes;
   std::vector<uintptr_t> cut{h0};   // piece i = [cut[i], cut[i + 1])
   for (uintptr_t c = (h0 + kPiece) & ~((uintptr_t{2} << 20) - 1); c < h1; c += kPiece)
@@ -1019,6 +1025,15 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
     }
   });
   int rc = kOk;
+  int waited = -1;   // parts whose event `s` already waits for: [0, waited]
+  auto wait_parts = [&](size_t end) {
+    int j = waited + 1;
+    while (j < nparts - 1 && ends[j] < end) ++j;
+    if (j >= nparts || j <= waited) return;
+    const hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)events[j], 0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+    waited = j;
+  };
   size_t i = 0;
   for (; i < n && rc == kOk; ++i) {
     int st;
@@ -1030,6 +1045,8 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
     if (st < 0) break;
     for (uintptr_t off = cut[i]; off < cut[i + 1] && rc == kOk; off += kStagedChunk) {
       const size_t len = cut[i + 1] - off < kStagedChunk ? cut[i + 1] - off : kStagedChunk;
+      wait_parts(off + len - h0);
+      if (rc != kOk) break;
       if (before) before(ctx, off + len - h0);
       const hipError_t e = hipMemcpyAsync(reinterpret_cast<char*>(off), d + (off - h0), len,
                                           hipMemcpyDeviceToHost, s);
@@ -1043,7 +1060,8 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
     const size_t off = cut[i] - h0;
     prefault(h + off, bytes - off, 8);
     if (before) before(ctx, bytes);
-    rc = bounce_d2h(h + off, d + off, bytes - off, s);
+    wait_parts(bytes);
+    if (rc == kOk) rc = bounce_d2h(h + off, d + off, bytes - off, s);
   }
   const hipError_t e = hipStreamSynchronize(s);
   if (rc == kOk && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
@@ -1143,6 +1161,20 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
 int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
                               void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
                               void* stream) {
+  return dpf_hip_memcpy_d2h_staged_after(dst, src, bytes, before_chunk, ctx, 0, nullptr, nullptr,
+                                         stream);
+}
+int dpf_hip_memcpy_d2h_staged_after(void* dst, const void* src, size_t bytes,
+                                    void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
+                                    int num_parts, void* const* part_events,
+                                    const size_t* part_end_bytes, void* stream) {
+  if (num_parts < 0 || (num_parts > 0 && (!part_events || !part_end_bytes)))
+    return fail(kInvalidArgument, "dpf_hip_memcpy_d2h_staged_after: bad parts");
+  for (int j = 0; j < num_parts; ++j)
+    if (!part_events[j] || (j > 0 && part_end_bytes[j] < part_end_bytes[j - 1]) ||
+        (j == num_parts - 1 && part_end_bytes[j] < bytes))
+      return fail(kInvalidArgument, "dpf_hip_memcpy_d2h_staged_after: bad parts");
+  // Every path but the pipelined one copies on `stream`, after all its parts.
   if (!before_chunk) return dpf_hip_memcpy_d2h(dst, src, bytes, stream);
   uintptr_t base = 0;
   if (bytes >= kRegisterMin) {
@@ -1154,9 +1186,17 @@ int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
       return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, before_chunk,
                              ctx, (hipStream_t)stream, base);
     if (a == kNotOurs && !locked) {
-      if (d2h_pipeline_on())
-        return pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx,
-                             (hipStream_t)stream);
+      if (d2h_pipeline_on()) {
+        if (num_parts == 0)
+          return pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx,
+                               (hipStream_t)stream);
+        hipStream_t copy;
+        HIP_TRY(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking));
+        const int rc = pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx, copy,
+                                     num_parts, part_events, part_end_bytes);
+        (void)hipStreamDestroy(copy);
+        return rc;
+      }
       prefault((char*)dst, bytes, 16);
       if (acquire_host(dst, bytes, false, &base) == kAcquired)
         return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true,

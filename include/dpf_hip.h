@@ -119,6 +119,19 @@ int dpf_hip_memcpy_d2h_chunked(const void* src, size_t bytes, size_t align,
 int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
                               void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
                               void* stream);
+/* _staged for a source produced in parts on `stream`: [0, part_end_bytes[j])
+ * of `src` is complete once part_events[j] (dpf_hip_event_record on `stream`)
+ * has completed (ends non-decreasing, the last >= bytes).  A fresh pageable
+ * `dst` of >= DPF_HIP_REGISTER_MIN_BYTES is copied on a stream of the call's
+ * own, each DMA chunk waiting on the device for the first part that covers
+ * it, so the copy of part j overlaps the kernels producing the later parts;
+ * every other destination is copied on `stream` after all parts.  The
+ * drop-in EvaluateUntil<T> returns a >= 512 MiB first-call output this way,
+ * its expansion launched as 8 subtrees. */
+int dpf_hip_memcpy_d2h_staged_after(void* dst, const void* src, size_t bytes,
+                                    void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
+                                    int num_parts, void* const* part_events,
+                                    const size_t* part_end_bytes, void* stream);
 int dpf_hip_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int dpf_hip_memset(void* dst, int value, size_t bytes, void* stream);
 int dpf_hip_stream_sync(void* stream);

@@ -390,7 +390,8 @@ def test_large_host_output_matches_device(log, vt):
 
 @pytest.mark.parametrize("env", [{}, {"DPF_HIP_D2H_REGISTER_PIECES": "1"},
                                  {"DPF_HIP_D2H_REGISTER_PIECES": "0"},
-                                 {"DPF_HIP_D2H_PIPELINE": "0"}], ids=str)
+                                 {"DPF_HIP_D2H_PIPELINE": "0"}, {"DPF_EVAL_SPLIT": "0"},
+                                 {"DPF_EVAL_SPLIT": "0", "DPF_HIP_D2H_PIPELINE": "0"}], ids=str)
 def test_pipelined_host_output_and_its_fallbacks(env, monkeypatch):
     """A fresh host output of >= 512 MiB is mapped and registered in 256 MiB
     pieces by a helper thread while the DMA fills the pieces already
@@ -398,7 +399,9 @@ def test_pipelined_host_output_and_its_fallbacks(env, monkeypatch):
     the vector starts off a 2 MiB boundary) equals the device output byte for
     byte by default, when the registration of piece 1 or 0 and every later one
     is refused (the rest of the range through the bounce buffers), and with
-    the pipeline off (map and register the whole range first).  The hooks are
+    the pipeline off (map and register the whole range first).  By default
+    the expansion itself runs as 8 subtree launches whose events the copy
+    waits for part by part (DPF_EVAL_SPLIT=0: one launch).  The hooks are
     read per call."""
     import torch
     for k, v in env.items():
@@ -411,6 +414,36 @@ def test_pipelined_host_output_and_its_fallbacks(env, monkeypatch):
     dpf.evaluate_until_to_device(0, [], dpf.create_evaluation_context(k0), dev)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(dev.cpu().numpy().reshape(host.shape), host)
+
+
+def test_split_first_call_then_next_level():
+    """A first call whose >= 512 MiB host output is expanded as 8 subtree
+    launches leaves the context as one launch does: the next level's call
+    (from its prefixes) equals the device path's, and both levels reconstruct
+    the point function with the other party's key."""
+    import torch
+    dpf = E.params([(26, ("int", 64), 0), (27, ("int", 64), 0)])
+    alpha = (1 << 27) - 4321
+    k0, k1 = E.generate_keys(dpf, alpha, [[3], [4]], (71, 72))
+    prefixes = [alpha >> 1, 17, (1 << 26) - 1]
+    got = []
+    for key in (k0, k1):
+        ctx = dpf.create_evaluation_context(key)
+        h0 = dpf.evaluate_until(0, [], ctx, packed=True)
+        h1 = dpf.evaluate_until(1, prefixes, ctx, packed=True)
+        ctx_d = dpf.create_evaluation_context(key)
+        dev = torch.empty(h0.size, dtype=torch.uint8, device="cuda")
+        dpf.evaluate_until_to_device(0, [], ctx_d, dev)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dev.cpu().numpy().reshape(h0.shape), h0)
+        del dev
+        np.testing.assert_array_equal(h1, dpf.evaluate_until(1, prefixes, ctx_d, packed=True))
+        got.append((h0, h1))
+    vt = ("int", 64)
+    t0 = O.add_packed(vt, got[0][0], got[1][0])
+    assert np.flatnonzero(t0.any(axis=1)).tolist() == [alpha >> 1]
+    t1 = O.add_packed(vt, got[0][1], got[1][1])
+    assert np.flatnonzero(t1.any(axis=1)).tolist() == [2 * 0 + (alpha & 1)]
 
 
 def test_concurrent_pipelined_host_outputs():
