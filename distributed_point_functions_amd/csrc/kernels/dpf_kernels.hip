@@ -654,11 +654,142 @@ int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf
   return launch_expand(p, FastIntLeaf<BITS, false>{vcw, E, party, store_bytes, {}}, s);
 }
 
+// Integer leaves, four path chains per lane (ILP4): item u covers key grp and
+// the points q + j * quarter, j < 4 (p.half holds the quarter).  Same
+// arithmetic as eval_points_kernel<GenericLeaf, BITS, true, ...>, one more
+// pair of chains in flight per wave (points_ilp below picks it).
+template <int BITS, bool UNIFORM, bool SUM>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(PointParams p) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const int L = p.num_levels;
+  const int64_t P = p.points_per_key, quarter = p.half;
+  // Sums of <= 64-bit values wrap mod 2^64 exactly (the group is mod 2^BITS).
+  using Acc = typename std::conditional<(BITS <= 64), uint64_t, u128>::type;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
+       u += (int64_t)gridDim.x * blockDim.x) {
+    int64_t grp = u / quarter;
+    if (UNIFORM) grp = (int64_t)__builtin_amdgcn_readfirstlane((int)grp);
+    const int64_t q0 = u - grp * quarter;
+    // Point i of the item: q0 + i * quarter (clamped to q0 past the key's last point).
+    auto qi = [&](int i) { return q0 + i * quarter < P ? q0 + i * quarter : q0; };
+    auto pidx = [&](int i) { return p.shared_points ? qi(i) : grp * P + qi(i); };
+    int64_t k_begin = grp, k_end = grp + 1;
+    if (SUM) {
+      k_begin = grp * p.chunk_keys;
+      k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
+    }
+    Block4 path[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) path[i] = load_block(p.tree_index + pidx(i));
+    Acc acc[4] = {0, 0, 0, 0};
+    for (int64_t k = k_begin; k < k_end; ++k) {
+      const int party = p.party[k] & 1;
+      Block4 st[4];
+      uint32_t t[4];
+      if (p.seeds_in) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          st[i] = load_block(p.seeds_in + k * P + qi(i));
+          t[i] = p.ctrl_in[k * P + qi(i)] & 1u;
+        }
+      } else {
+        const Block4 root = load_block(p.key_seed + k);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          st[i] = root;
+          t[i] = (uint32_t)party;
+        }
+      }
+      const dpf_block* cws = p.cw_seed + k * p.cw_stride;
+      const uint8_t* cl = p.cw_left + k * p.cw_stride;
+      const uint8_t* cr = p.cw_right + k * p.cw_stride;
+      for (int j = 0; j < L; ++j) {
+        const dpf_block c = cws[j];
+        const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
+        uint32_t b[4];
+        SelectRK rk[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          b[i] = path_bit(path[i], L - 1 - j + p.bib);
+          rk[i] = SelectRK{p.rkl.k, p.rkd.k, 0u - b[i]};
+        }
+        Block4 h[4] = {st[0], st[1], st[2], st[3]};
+        dpf_aes::mmo_hashN<4>(h, lk, rk);
+        const uint32_t cw[4] = {(uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
+                                (uint32_t)(c.high >> 32)};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t m = 0u - t[i];
+          h[i].w0 ^= cw[0] & m; h[i].w1 ^= cw[1] & m; h[i].w2 ^= cw[2] & m; h[i].w3 ^= cw[3] & m;
+          t[i] = (h[i].w0 & 1u) ^ (t[i] & ((cctl >> b[i]) & 1u));
+          h[i].w0 &= ~1u;
+          st[i] = h[i];
+        }
+      }
+      const dpf_block* vcw = p.vcw + k * p.vcw_stride;
+      const UniformRK vk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
+                               UniformRK{p.rkv.k}};
+      dpf_aes::mmo_hashN<4>(st, lk, vk);
+      const uint32_t bmask = (1u << p.bib) - 1u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int bi = p.block_index ? p.block_index[pidx(i)] : (int)(path[i].w0 & bmask);
+        const u128 v = fast_point_value<BITS>(st[i], t[i], bi, dpf_u128(vcw[bi]), party, p.xor_mode);
+        if (SUM)
+          acc[i] = p.xor_mode ? (acc[i] ^ (Acc)v) : (acc[i] + (Acc)v);
+        else if (q0 + i * quarter < P)
+          store_bits<BITS>(p.out + (k * P + qi(i)) * (int64_t)p.esz, v);
+      }
+    }
+    if (SUM && k_begin < k_end) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (q0 + i * quarter >= P) continue;
+        unsigned long long* w = p.wide + qi(i) * 3;
+        if (p.xor_mode) wide_xor(w, (u128)acc[i]); else wide_add(w, (u128)acc[i]);
+      }
+    }
+  }
+}
+
+// DPF_POINTS_ILP=2|4 (read per launch) forces two or four chains per lane
+// (four only where a quarter of a key's points is a whole number of waves);
+// by default integer leaves take four chains when the launch fills every CU
+// with 1024-thread workgroups (config 4: +0.7% per key, +1.4% summed over
+// keys, profiles/r14_ab.txt) and two otherwise.
+int points_ilp() {
+  const char* v = std::getenv("DPF_POINTS_ILP");
+  return v && (v[0] == '2' || v[0] == '4') ? v[0] - '0' : 0;
+}
+thread_local const char* g_last_points_kernel = "";
+
 template <class Leaf, int BITS, bool FAST, bool SUM>
 int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
+  if constexpr (FAST) {
+    // ILP4: quarter = ceil(P / 4) points per chain row; enough items to fill the chip.
+    const int64_t quarter = (pp.points_per_key + 3) / 4;
+    const int64_t items = SUM ? pp.num_items / pp.half * quarter : pp.num_keys * quarter;
+    const int ilp = points_ilp();
+    if (quarter % 64 == 0 &&
+        (ilp == 4 || (ilp == 0 && items >= (int64_t)num_cus() * 1024))) {
+      g_last_points_kernel = "points/ilp4";
+      PointParams p = pp;
+      p.half = quarter;
+      p.num_items = items;
+      const int blk = block_for(p.num_items);
+      hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM>), dim3(grid_for(p.num_items, blk)),
+                         dim3(blk), 0, s, p);
+      HIP_TRY(hipGetLastError());
+      return kOk;
+    }
+  }
   if constexpr (!SUM) {
     // Fewer paired items than one wave per CU: latency-bound, run unpaired.
-    if (pp.num_items < (int64_t)num_cus() * 64) {
+    if (pp.num_items < (int64_t)num_cus() * 64 && points_ilp() != 2) {
+      g_last_points_kernel = "points/single";
       PointParams p = pp;
       p.half = p.points_per_key;
       p.num_items = p.num_keys * p.points_per_key;
@@ -674,6 +805,7 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
       return kOk;
     }
   }
+  g_last_points_kernel = "points/ilp2";
   const PointParams& p = pp;
   const int blk = block_for(p.num_items);
   const dim3 grid(grid_for(p.num_items, blk)), block(blk);
@@ -758,6 +890,7 @@ extern "C" {
 int dpf_hip_abi_version(void) { return DPF_HIP_ABI_VERSION; }
 const char* dpf_hip_last_error(void) { return dpf_rt::g_last_error.c_str(); }
 
+const char* dpf_hip_last_points_kernel(void) { return g_last_points_kernel; }
 const char* dpf_hip_last_expand_kernel(int* subtree_depth) {
   if (subtree_depth) *subtree_depth = dpf_rt::g_last_expand_s;
   return dpf_rt::g_last_expand;

@@ -78,6 +78,8 @@ def load(require_gpu: bool = False):
         L.dpf_hip_last_expand_kernel.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.dpf_hip_last_batch_kernel.restype = ctypes.c_char_p
         L.dpf_hip_last_batch_kernel.argtypes = []
+        L.dpf_hip_last_points_kernel.restype = ctypes.c_char_p
+        L.dpf_hip_last_points_kernel.argtypes = []
         L.dpf_hip_hash.argtypes = [I64, P, P, P, P]
         L.dpf_hip_eval_paths.argtypes = [I64, I, P, P, P, P, P, P, P, P, P, P, P]
         L.dpf_hip_expand.argtypes = [I64, P, P, I, P, P, P, P, P, P, P, I, P, I, P, P]
@@ -111,6 +113,12 @@ def last_batch_kernel() -> str:
     """Kernel of this thread's last batched prefix evaluation, e.g. "hh_level"
     -- dispatch diagnostics for the tests."""
     return load().dpf_hip_last_batch_kernel().decode()
+
+
+def last_points_kernel() -> str:
+    """Kernel of this thread's last point evaluation, e.g. "points/ilp4" --
+    dispatch diagnostics for the tests."""
+    return load().dpf_hip_last_points_kernel().decode()
 
 
 def check(st: int):

@@ -195,6 +195,12 @@ const char* dpf_hip_last_expand_kernel(int* subtree_depth);
  * "batch_level/generic"; "" before the first call. */
 const char* dpf_hip_last_batch_kernel(void);
 
+/* Diagnostic: which point kernel the calling thread's last point evaluation
+ * (dpf_hip_eval_points*, per key or summed) launched: "points/ilp4" (integer
+ * leaves, four path chains per lane), "points/ilp2" (two) or "points/single"
+ * (one, for launches below one wave per CU); "" before the first call. */
+const char* dpf_hip_last_points_kernel(void);
+
 /* ---- a11: fused point evaluation for many keys ----------------------------
  * Replaces EvaluateAtImpl's path walk + hash + correction (h:930-1003).
  * Point i belongs to key k = i / points_per_key.  Its walk starts at

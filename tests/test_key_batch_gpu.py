@@ -173,3 +173,81 @@ def test_batch_range_upload_and_errors():
     with pytest.raises(D.DpfStatusError) as e:
         other.evaluate_at_batch_to_device(part, 0, _dev_points(pts), 8, out)
     assert e.value.message == "key batch does not match this DistributedPointFunction"
+
+
+ILP_CASES = [
+    # (levels, keys, points per key): a quarter of the points a whole number of waves
+    ([(128, ("int", 64), 0)], 6, 256),
+    ([(40, ("int", 128), 0)], 3, 512),
+    ([(64, ("xor", 128), 0)], 3, 256),
+    ([(30, ("int", 8), 0)], 4, 256),                 # 16 elements per block
+    ([(10, ("int", 16), 0), (50, ("int", 64), 0)], 4, 256),
+]
+
+
+@pytest.mark.parametrize("ilp", ["4", "2"])
+@pytest.mark.parametrize("levels,n_keys,ppk", ILP_CASES, ids=str)
+def test_points_kernel_chains_per_lane(levels, n_keys, ppk, ilp, monkeypatch):
+    """Integer point evaluation with four path chains per lane
+    (eval_points4_kernel, the default for launches that fill the chip) and with
+    two (eval_points_kernel), forced through DPF_POINTS_ILP: per-key points,
+    shared points and the key sum all equal the oracle, and the dispatch
+    diagnostic names the kernel that ran."""
+    import torch
+    from distributed_point_functions_amd import hip_abi as H
+    monkeypatch.setenv("DPF_POINTS_ILP", ilp)
+    h = len(levels) - 1
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=ppk + int(ilp))
+    vt, log = levels[h][1], levels[h][0]
+    dev_batch = dpf.upload_key_batch(batch)
+    size = dpf.packed_size(h)
+    pts = _rand_u128(rng, n_keys * ppk, log)
+    out = torch.empty(n_keys * ppk * size, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_to_device(dev_batch, h, _dev_points(pts), ppk, out)
+    torch.cuda.synchronize()
+    assert H.last_points_kernel() == f"points/ilp{ilp}"
+    got = out.cpu().numpy().reshape(n_keys * ppk, size)
+    for k in range(n_keys):
+        np.testing.assert_array_equal(got[k * ppk:(k + 1) * ppk],
+                                      O.evaluate_at(P, oks[k], h, pts[k * ppk:(k + 1) * ppk]),
+                                      err_msg=f"key {k}")
+    shared = pts[:ppk]
+    dpf.evaluate_at_batch_to_device(dev_batch, h, _dev_points(shared), ppk, out, shared_points=True)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(n_keys, ppk, size)
+    want = [O.evaluate_at(P, oks[k], h, shared) for k in range(n_keys)]
+    for k in range(n_keys):
+        np.testing.assert_array_equal(got[k], want[k])
+    sums = torch.empty(ppk * size, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_sum_to_device(dev_batch, h, _dev_points(shared), sums)
+    torch.cuda.synchronize()
+    assert H.last_points_kernel() == f"points/ilp{ilp}"
+    total = want[0]
+    for k in range(1, n_keys):
+        total = O.add_packed(vt, total, want[k])
+    np.testing.assert_array_equal(sums.cpu().numpy().reshape(ppk, size), total)
+
+
+def test_points_kernel_default_dispatch():
+    """Without the hook, a launch that fills every CU with 1024-thread
+    workgroups takes four chains per lane; a smaller one takes two (and one
+    below a wave of point pairs per CU)."""
+    import torch
+    from distributed_point_functions_amd import hip_abi as H
+    levels = [(64, ("int", 64), 0)]
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, 1024, seed=5)
+    dev_batch = dpf.upload_key_batch(batch)
+    pts = _rand_u128(rng, 1024, 64)
+    out = torch.empty(1024 * 1024 * 8, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_to_device(dev_batch, 0, _dev_points(pts), 1024, out, shared_points=True)
+    torch.cuda.synchronize()
+    assert H.last_points_kernel() == "points/ilp4"
+    got = out.cpu().numpy().reshape(1024, 1024, 8)
+    for k in (0, 1, 511, 1023):
+        np.testing.assert_array_equal(got[k], O.evaluate_at(P, oks[k], 0, pts), err_msg=f"key {k}")
+    # 128 keys x 256 points: a wave per CU of point pairs, not a full chip of quads.
+    small = torch.empty(128 * 256 * 8, dtype=torch.uint8, device="cuda")
+    sub = dpf.upload_key_batch(batch, 0, 128)
+    dpf.evaluate_at_batch_to_device(sub, 0, _dev_points(pts[:256]), 256, small, shared_points=True)
+    torch.cuda.synchronize()
+    assert H.last_points_kernel() == "points/ilp2"
