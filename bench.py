@@ -719,6 +719,7 @@ def main_evaluate_at(args):
         total = step(evs[i])
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    timed_kernel = H.last_points_kernel()   # before the spot checks launch their own
     if world > 1:
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
@@ -748,8 +749,13 @@ def main_evaluate_at(args):
     depth = dpf.hierarchy_to_tree()[0]                 # 127 path levels, + 1 value hash
     aes_per_launch = nk * ppk * (depth + 1)
     achieved = aes_per_launch / (kern_ms_max * 1e-3) / 1e9
-    kname = ("eval_points_kernel<(anonymous namespace)::GenericLeaf, 64, true, true, %s" %
-             ("true>" if summed else "false, true>"))
+    # The point kernel the timed launches ran (dpf_hip_last_points_kernel):
+    # four path chains per lane at this size, two otherwise.
+    if timed_kernel == "points/ilp4":
+        kname = "eval_points4_kernel<64, true, %s>" % ("true" if summed else "false")
+    else:
+        kname = ("eval_points_kernel<(anonymous namespace)::GenericLeaf, 64, true, true, %s" %
+                 ("true>" if summed else "false, true>"))
     tr = (profiled_traffic(kname, workload=args.workload)
           if n_keys == 1 << 20 and ppk == 1 << 10 and world == 1 else None)
     if rank == 0:

@@ -59,8 +59,8 @@ part2)
   profline full_domain_tuple_u32x2 "expand_octet_kernel<FastIntLeaf<32, false> >" launch:2 tuple_u32 "--steps 10 --warmup 2 --no-cpu-baseline" --workload full_domain_tuple --tuple-type u32x2
   ;;
 part3)
-  profline evaluate_at "eval_points_kernel" launch:1 evaluate_at "--steps 3 --warmup 1 --no-cpu-baseline" --workload evaluate_at
-  profline evaluate_at_sum "eval_points_kernel" launch:1 evaluate_at_sum "--steps 3 --warmup 1 --no-cpu-baseline" --workload evaluate_at_sum
+  profline evaluate_at "eval_points4_kernel" launch:1 evaluate_at "--steps 3 --warmup 1 --no-cpu-baseline" --workload evaluate_at
+  profline evaluate_at_sum "eval_points4_kernel" launch:1 evaluate_at_sum "--steps 3 --warmup 1 --no-cpu-baseline" --workload evaluate_at_sum
   profline dcf "dcf_fast_kernel" launch:2 dcf "--steps 10 --warmup 2 --no-cpu-baseline" --workload dcf
   ;;
 part4)
