@@ -1,0 +1,47 @@
+"""bench.py's N-rank path on the GPU (the driver's scaling runs launch it as
+`torch.distributed.run --nproc-per-node N bench.py --gpus N`).
+
+RCCL refuses two ranks on one device, so DPF_BENCH_ONE_GPU=1 puts both ranks
+on cuda:0 with a gloo group (bench.py: init_ranks): each rank evaluates its own
+2^30-output shard of config 2 (weak scaling, no data-path collective), the
+barrier and the max-over-ranks timing are the ones the 8-GPU run uses, and
+rank 0 prints one line whose `value` counts the outputs of both ranks.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_ranks_on_one_gpu_weak_scaling_line():
+    env = dict(os.environ, DPF_BENCH_ONE_GPU="1", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]   # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["scaling"] == "weak"
+    pg = d["process_group"]
+    assert pg["world_size"] == 2 and pg["backend"] == "gloo"
+    assert len(pg["kernel_ms_per_rank"]) == 2
+    # value = outputs of all ranks / max-over-ranks time of the timed steps.
+    outputs = 2 * d["config"]["outputs_per_gpu"]
+    assert d["value"] == pytest.approx(outputs / (d["ms_per_step"] * 1e-3), rel=1e-6)
+    assert d["roofline"]["frac"] > 0
