@@ -1180,7 +1180,15 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
       const size_t len = cut[i + 1] - off < kStagedChunk ? cut[i + 1] - off : kStagedChunk;
       wait_parts(off + len - h0);
       if (rc != kOk) break;
-      if (before) before(ctx, off + len - h0);
+      if (before) {
+        // The helper thread must be joined on every path out of here.
+        try {
+          before(ctx, off + len - h0);
+        } catch (...) {
+          rc = fail(kInternal, "dpf_hip_memcpy_d2h_staged: before_chunk threw");
+          break;
+        }
+      }
       const hipError_t e = hipMemcpyAsync(reinterpret_cast<char*>(off), d + (off - h0), len,
                                           hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync (registered host memory)");
@@ -1192,8 +1200,12 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
     // Registration refused from piece i on: the rest through the bounce buffers.
     const size_t off = cut[i] - h0;
     prefault(h + off, bytes - off, 8);
-    if (before) before(ctx, bytes);
-    wait_parts(bytes);
+    try {
+      if (before) before(ctx, bytes);
+    } catch (...) {
+      rc = fail(kInternal, "dpf_hip_memcpy_d2h_staged: before_chunk threw");
+    }
+    if (rc == kOk) wait_parts(bytes);
     if (rc == kOk) rc = bounce_d2h(h + off, d + off, bytes - off, s);
   }
   const hipError_t e = hipStreamSynchronize(s);
