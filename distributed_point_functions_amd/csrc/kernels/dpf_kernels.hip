@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <mutex>
@@ -1070,7 +1071,7 @@ int registered_copy(char* h, char* d, size_t bytes, bool to_host, void (*before)
 void prefault(char* p, size_t bytes, int threads) {
   constexpr size_t kPage = 4096;
   const size_t pages = bytes / kPage + 1;
-  size_t t = bytes >> 25;   // one thread per 32 MiB
+  size_t t = bytes >> 24;   // one thread per 16 MiB
   if (t > static_cast<size_t>(threads)) t = threads;
   auto touch = [p, bytes](size_t lo, size_t hi) {
     volatile char* v = p;
@@ -1086,12 +1087,15 @@ void prefault(char* p, size_t bytes, int threads) {
   for (auto& th : pool) th.join();
 }
 
-// DPF_HIP_D2H_PIPELINE=0 (read per call): a fresh destination of >=
-// kRegisterMin is mapped and registered whole before the first DMA (the r13
-// path), instead of piece by piece behind the DMA.  An A/B hook.
-bool d2h_pipeline_on() {
+// A fresh destination of kRegisterMin..kPipelineMax is mapped and registered
+// piece by piece behind the DMA; a larger one whole before the first DMA (the
+// r13 path).  DPF_HIP_D2H_PIPELINE=0 / =1 (read per call) forces either: A/B
+// and test hooks.
+constexpr size_t kPipelineMax = size_t{16} << 30;   // see piece_bytes below
+bool d2h_pipeline_on(size_t bytes) {
   const char* v = std::getenv("DPF_HIP_D2H_PIPELINE");
-  return !(v && v[0] == '0');
+  if (v && v[0] == '1') return true;   // force (probes)
+  return !(v && v[0] == '0') && bytes <= kPipelineMax;
 }
 // DPF_HIP_D2H_REGISTER_PIECES=<n> (read per call): the pipelined copy acts as
 // if the registration of its piece n (and every later one) were refused -- a
@@ -1103,13 +1107,36 @@ long register_pieces_limit() {
 
 // A fresh pageable destination of >= kRegisterMin (no registration of ours
 // overlaps it): a helper thread maps (prefault, 8 threads) and registers it in
-// 256 MiB pieces while this thread initialises (before) and DMAs the pieces
+// pieces (256 MiB, or 1/32 of the range) while this thread initialises (before) and DMAs the pieces
 // already registered, so the ~45 ms of mapping and registering 8 GiB runs
 // under the DMA instead of ahead of it.  Piece boundaries are 2 MiB-aligned
 // (no page in two registrations) and every DMA chunk lies in one piece.  A
 // piece whose registration is refused, and everything after it, goes through
 // the bounce buffers.
 constexpr size_t kPiece = size_t{256} << 20;
+// At most ~32 pieces (256 MiB up to 8 GiB), and only up to kPipelineMax: a
+// 32 GiB copy (config 3's 2^31 uint128) ran 1.0-1.45 s pipelined, but in 1 of
+// 4 calls its DMA alone took ~2.65 s (13 GB/s; the helper thread never
+// behind, the value-initialisation on the calling thread 1.0-1.4 s either
+// way), with 129 pieces or 33; mapped and registered whole first it ran
+// 1.27-1.62 s in every call (profiles/r14_u128_reps_probe.txt).  8 GiB copies
+// never showed the slow mode (164-171 ms pipelined vs 199-209 ms).  A/B hooks
+// (read per call): DPF_HIP_D2H_PIECE_MIB (a multiple of 64) and
+// DPF_HIP_D2H_PREFAULT_THREADS (default 8).
+
+size_t piece_bytes(size_t bytes) {
+  const char* v = std::getenv("DPF_HIP_D2H_PIECE_MIB");
+  const long m = v && *v ? std::strtol(v, nullptr, 10) : 0;
+  if (m >= 64 && m % 64 == 0) return static_cast<size_t>(m) << 20;
+  const size_t step = size_t{64} << 20;
+  const size_t want = (bytes / 32 + step - 1) / step * step;
+  return want > kPiece ? want : kPiece;
+}
+int prefault_threads() {
+  const char* v = std::getenv("DPF_HIP_D2H_PREFAULT_THREADS");
+  const long t = v && *v ? std::strtol(v, nullptr, 10) : 0;
+  return t >= 1 && t <= 64 ? static_cast<int>(t) : 8;
+}
 
 // With parts (nparts > 0) the DMAs run on `s` = a copy stream of their own:
 // [0, ends[j]) of `d` is ready once events[j] (recorded on the producing
@@ -1120,8 +1147,10 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
                   hipStream_t s, int nparts = 0, void* const* events = nullptr,
                   const size_t* ends = nullptr) {
   const uintptr_t h0 = reinterpret_cast<uintptr_t>(h), h1 = h0 + bytes;
+  const size_t piece = piece_bytes(bytes);
+  const int pf_threads = prefault_threads();
   std::vector<uintptr_t> cut{h0};   // piece i = [cut[i], cut[i + 1])
-  for (uintptr_t c = (h0 + kPiece) & ~((uintptr_t{2} << 20) - 1); c < h1; c += kPiece)
+  for (uintptr_t c = (h0 + piece) & ~((uintptr_t{2} << 20) - 1); c < h1; c += piece)
     if (c > cut.back()) cut.push_back(c);
   cut.push_back(h1);
   const size_t n = cut.size() - 1;
@@ -1132,12 +1161,20 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
   int device = 0;
   (void)hipGetDevice(&device);
   const long limit = register_pieces_limit();
+  // DPF_HIP_D2H_TRACE=1: per-call seconds spent mapping, registering and
+  // waiting for the helper thread, on stderr (a diagnostic).
+  const bool trace = std::getenv("DPF_HIP_D2H_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  double t_fault = 0, t_reg = 0, t_wait = 0, t_before = 0;
+  const auto t_start = clk::now();
   std::thread worker([&] {
     (void)hipSetDevice(device);
     for (size_t i = 0; i < n && !stop.load(); ++i) {
       char* p = reinterpret_cast<char*>(cut[i]);
       const size_t len = cut[i + 1] - cut[i];
-      prefault(p, len, 8);
+      const auto a = clk::now();
+      prefault(p, len, pf_threads);
+      const auto b = clk::now();
       int st = -1;
       if (limit >= 0 && static_cast<long>(i) >= limit) {
         // test hook: refused
@@ -1149,6 +1186,8 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
       } else {
         (void)hipGetLastError();
       }
+      t_fault += std::chrono::duration<double>(b - a).count();
+      t_reg += std::chrono::duration<double>(clk::now() - b).count();
       {
         std::lock_guard<std::mutex> lock(mu);
         state[i] = st;
@@ -1171,9 +1210,11 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
   for (; i < n && rc == kOk; ++i) {
     int st;
     {
+      const auto w = clk::now();
       std::unique_lock<std::mutex> lock(mu);
       cv.wait(lock, [&] { return state[i] != 0; });
       st = state[i];
+      t_wait += std::chrono::duration<double>(clk::now() - w).count();
     }
     if (st < 0) break;
     for (uintptr_t off = cut[i]; off < cut[i + 1] && rc == kOk; off += kStagedChunk) {
@@ -1183,7 +1224,9 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
       if (before) {
         // The helper thread must be joined on every path out of here.
         try {
+          const auto bt = clk::now();
           before(ctx, off + len - h0);
+          t_before += std::chrono::duration<double>(clk::now() - bt).count();
         } catch (...) {
           rc = fail(kInternal, "dpf_hip_memcpy_d2h_staged: before_chunk threw");
           break;
@@ -1208,10 +1251,21 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
     if (rc == kOk) wait_parts(bytes);
     if (rc == kOk) rc = bounce_d2h(h + off, d + off, bytes - off, s);
   }
+  const auto t_issue = clk::now();
   const hipError_t e = hipStreamSynchronize(s);
   if (rc == kOk && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+  const auto t_sync = clk::now();
   for (size_t j = 0; j < n; ++j)
     if (state[j] > 0) release_host(cut[j]);
+  if (trace)
+    fprintf(stderr, "[pipelined_d2h] %zu MiB in %zu pieces: total %.1f ms, map %.1f ms, register "
+            "%.1f ms (helper), wait %.1f ms, before_chunk %.1f ms, issue %.1f ms, final sync "
+            "%.1f ms, unregister %.1f ms\n", bytes >> 20, n,
+            1e3 * std::chrono::duration<double>(clk::now() - t_start).count(), 1e3 * t_fault,
+            1e3 * t_reg, 1e3 * t_wait, 1e3 * t_before,
+            1e3 * std::chrono::duration<double>(t_issue - t_start).count(),
+            1e3 * std::chrono::duration<double>(t_sync - t_issue).count(),
+            1e3 * std::chrono::duration<double>(clk::now() - t_sync).count());
   return rc;
 }
 
@@ -1331,7 +1385,7 @@ int dpf_hip_memcpy_d2h_staged_after(void* dst, const void* src, size_t bytes,
       return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, before_chunk,
                              ctx, (hipStream_t)stream, base);
     if (a == kNotOurs && !locked) {
-      if (d2h_pipeline_on()) {
+      if (d2h_pipeline_on(bytes)) {
         if (num_parts == 0)
           return pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx,
                                (hipStream_t)stream);
