@@ -1083,7 +1083,13 @@ void prefault(char* p, size_t bytes, int threads) {
     return;
   }
   std::vector<std::thread> pool;
-  for (size_t i = 0; i < t; ++i) pool.emplace_back(touch, pages * i / t, pages * (i + 1) / t);
+  size_t done = 0;   // ranges [0, done) handed to threads
+  try {
+    for (; done < t; ++done) pool.emplace_back(touch, pages * done / t, pages * (done + 1) / t);
+  } catch (...) {
+    // No thread to spare: the rest on this one.
+  }
+  if (done < t) touch(pages * done / t, pages);
   for (auto& th : pool) th.join();
 }
 
@@ -1114,6 +1120,7 @@ long register_pieces_limit() {
 // piece whose registration is refused, and everything after it, goes through
 // the bounce buffers.
 constexpr size_t kPiece = size_t{256} << 20;
+constexpr int kNoHelperThread = -1000;   // pipelined_d2h could not start its helper
 // At most ~32 pieces (256 MiB up to 8 GiB), and only up to kPipelineMax: a
 // 32 GiB copy (config 3's 2^31 uint128) ran 1.0-1.45 s pipelined, but in 1 of
 // 4 calls its DMA alone took ~2.65 s (13 GB/s; the helper thread never
@@ -1167,7 +1174,8 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
   using clk = std::chrono::steady_clock;
   double t_fault = 0, t_reg = 0, t_wait = 0, t_before = 0;
   const auto t_start = clk::now();
-  std::thread worker([&] {
+  std::thread worker;
+  auto helper = [&] {
     (void)hipSetDevice(device);
     for (size_t i = 0; i < n && !stop.load(); ++i) {
       char* p = reinterpret_cast<char*>(cut[i]);
@@ -1195,7 +1203,12 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
       cv.notify_all();
       if (st < 0) break;
     }
-  });
+  };
+  try {
+    worker = std::thread(helper);
+  } catch (...) {
+    return kNoHelperThread;   // nothing done yet: the caller copies another way
+  }
   int rc = kOk;
   int waited = -1;   // parts whose event `s` already waits for: [0, waited]
   auto wait_parts = [&](size_t end) {
@@ -1386,15 +1399,19 @@ int dpf_hip_memcpy_d2h_staged_after(void* dst, const void* src, size_t bytes,
                              ctx, (hipStream_t)stream, base);
     if (a == kNotOurs && !locked) {
       if (d2h_pipeline_on(bytes)) {
-        if (num_parts == 0)
-          return pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx,
-                               (hipStream_t)stream);
-        hipStream_t copy;
-        HIP_TRY(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking));
-        const int rc = pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx, copy,
-                                     num_parts, part_events, part_end_bytes);
-        (void)hipStreamDestroy(copy);
-        return rc;
+        int rc;
+        if (num_parts == 0) {
+          rc = pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx,
+                             (hipStream_t)stream);
+        } else {
+          hipStream_t copy;
+          HIP_TRY(hipStreamCreateWithFlags(&copy, hipStreamNonBlocking));
+          rc = pipelined_d2h((char*)dst, (const char*)src, bytes, before_chunk, ctx, copy,
+                             num_parts, part_events, part_end_bytes);
+          (void)hipStreamDestroy(copy);
+        }
+        if (rc != kNoHelperThread) return rc;
+        // No helper thread: map and register the whole range first.
       }
       prefault((char*)dst, bytes, 16);
       if (acquire_host(dst, bytes, false, &base) == kAcquired)
