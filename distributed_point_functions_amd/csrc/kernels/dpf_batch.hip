@@ -579,16 +579,30 @@ __global__ void sum_rows_kernel(int64_t rows, int64_t row_len, dpf_value_desc d,
 __global__ void gather_seeds_kernel(int64_t keys, int64_t T, const int64_t* __restrict__ slot,
                                     const dpf_block* __restrict__ cache, int64_t cache_stride,
                                     dpf_block* __restrict__ seeds_out,
-                                    uint8_t* __restrict__ ctrl_out) {
+                                    uint8_t* __restrict__ ctrl_out, int keys_per_lane) {
   // blockIdx.y walks the keys, blockIdx.x the rows: no division per element.
-  for (int64_t k = blockIdx.y; k < keys; k += gridDim.y) {
-    const dpf_block* row = cache + k * cache_stride;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < T;
-         i += (int64_t)gridDim.x * blockDim.x) {
-      Block4 c = load_block(row + slot[i]);
-      ctrl_out[k * T + i] = (uint8_t)(c.w0 & 1u);
-      c.w0 &= ~1u;
-      store_block(seeds_out + k * T + i, c);
+  // Up to four keys' loads are issued before their stores (the scattered
+  // 16-byte reads are latency-bound at one load in flight per lane).
+  constexpr int kKeys = 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < T;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t si = slot[i];
+    for (int64_t k0 = blockIdx.y; k0 < keys; k0 += (int64_t)gridDim.y * keys_per_lane) {
+      Block4 c[kKeys];
+#pragma unroll
+      for (int j = 0; j < kKeys; ++j) {
+        const int64_t k = k0 + j * (int64_t)gridDim.y;
+        if (j < keys_per_lane && k < keys) c[j] = load_block(cache + k * cache_stride + si);
+      }
+#pragma unroll
+      for (int j = 0; j < kKeys; ++j) {
+        const int64_t k = k0 + j * (int64_t)gridDim.y;
+        if (j < keys_per_lane && k < keys) {
+          ctrl_out[k * T + i] = (uint8_t)(c[j].w0 & 1u);
+          c[j].w0 &= ~1u;
+          store_block(seeds_out + k * T + i, c[j]);
+        }
+      }
     }
   }
 }
@@ -680,11 +694,16 @@ int dpf_hip_gather_seeds(int64_t num_keys, int64_t num_rows, const int64_t* slot
   if (!slot || !cache || !seeds_out || !control_out) return fail(kInvalidArgument, "NULL pointer");
   int64_t gx = (num_rows + 255) / 256;
   if (gx > 64) gx = 64;
-  int64_t gy = num_keys < 65535 ? num_keys : 65535;
+  // DPF_BATCH_GATHER_KEYS=1|2|4 (read per call; default 4): keys per lane and
+  // pass, an A/B hook.
+  const char* kv = getenv("DPF_BATCH_GATHER_KEYS");
+  const int kpl = kv && (kv[0] == '1' || kv[0] == '2') ? kv[0] - '0' : 4;
+  const int64_t ky = (num_keys + kpl - 1) / kpl;
+  int64_t gy = ky < 65535 ? ky : 65535;
   if (gx * gy > 262144) gy = (262144 + gx - 1) / gx;
   hipLaunchKernelGGL(gather_seeds_kernel, dim3((unsigned)gx, (unsigned)gy), dim3(256), 0,
                      (hipStream_t)stream,
-                     num_keys, num_rows, slot, cache, cache_stride, seeds_out, control_out);
+                     num_keys, num_rows, slot, cache, cache_stride, seeds_out, control_out, kpl);
   HIP_TRY(hipGetLastError());
   return kOk;
 }
