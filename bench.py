@@ -382,15 +382,80 @@ def aes_rooflines(achieved: float, kernel: str, **extra) -> dict:
     }
 
 
-def init_ranks(torch, dist):
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n: int, port: int) -> list:
+    """The torch.distributed.run command that runs this script as n ranks
+    (one process per GPU, rendezvous on 127.0.0.1) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+            "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def maybe_self_launch(args, argv=None) -> None:
+    """`python bench.py --gpus N` (N > 1) without a launcher: start the N ranks
+    as child processes of a torch.distributed.run launcher, relay rank 0's
+    JSON line, and exit with the launcher's status -- never fall back to one
+    rank.  Runs before anything touches the GPU (torch.cuda.device_count()
+    does not initialise HIP on this image; the children are started with
+    subprocess, not exec).  Fewer visible devices than N is an error, except
+    under DPF_BENCH_ONE_GPU=1 (every rank on cuda:0, the one-GPU rehearsal)."""
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least one GPU")
+    if args.workload.startswith("synthetic") and args.gpus != 1:
+        raise SystemExit("synthetic_* workloads evaluate one key on one GPU (--gpus 1)")
+    if "WORLD_SIZE" in os.environ:
+        ws = int(os.environ["WORLD_SIZE"])
+        if ws != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={ws}: the launcher started "
+                             f"{ws} ranks")
+        return
+    if args.gpus == 1:
+        return
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    need = 1 if os.environ.get("DPF_BENCH_ONE_GPU") == "1" else args.gpus
+    if have < need:
+        raise SystemExit(f"--gpus {args.gpus}: only {have} GPU(s) visible; refusing to run "
+                         f"fewer ranks than asked")
+    argv = sys.argv[1:] if argv is None else argv
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PYTHONUNBUFFERED="1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(launcher_cmd(argv, args.gpus, _free_port()), cwd=ROOT, env=env,
+                            stdout=subprocess.PIPE, text=True)
+    lines = 0
+    for line in proc.stdout:           # rank 0's JSON line; anything else goes to stderr
+        if line.startswith("{"):
+            lines += 1
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and lines != 1:
+        print(f"bench.py: expected one JSON line from rank 0, got {lines}", file=sys.stderr)
+        rc = 1
+    raise SystemExit(rc)
+
+
+def init_ranks(torch, dist, gpus: int = None):
     """One process per GPU (RANK/LOCAL_RANK/WORLD_SIZE from torch.distributed.run),
     RCCL process group for N > 1.  Returns (world, rank, local, coll), `coll`
-    the device for collective scalars (None: host tensors).
+    the device for collective scalars (None: host tensors).  `gpus` (the
+    --gpus flag) must equal the launcher's world size.
     DPF_BENCH_ONE_GPU=1 rehearses the N-rank path on a one-GPU box: every rank
     on cuda:0, a gloo group (RCCL refuses two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if gpus is not None and world != gpus:
+        raise SystemExit(f"--gpus {gpus} but {world} rank(s) running")
     one_gpu = os.environ.get("DPF_BENCH_ONE_GPU") == "1"
     if one_gpu:
         local = 0
@@ -407,6 +472,7 @@ def init_ranks(torch, dist):
 
 def main():
     args = parse()
+    maybe_self_launch(args)
     if args.workload.startswith("evaluate_at"):
         return main_evaluate_at(args)
     if args.workload.startswith("synthetic"):
@@ -424,9 +490,7 @@ def main():
     from distributed_point_functions_amd import proto as pb
     from distributed_point_functions_amd import sharding as S
 
-    if args.gpus != int(os.environ.get("WORLD_SIZE", "1")) and int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
-    world, rank, local, coll = init_ranks(torch, dist)
+    world, rank, local, coll = init_ranks(torch, dist, args.gpus)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -637,7 +701,7 @@ def main_evaluate_at(args):
     from distributed_point_functions_amd import proto as pb
     from distributed_point_functions_amd import sharding as S
 
-    world, rank, local, coll = init_ranks(torch, dist)
+    world, rank, local, coll = init_ranks(torch, dist, args.gpus)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -813,8 +877,8 @@ def main_synthetic(args):
     with the README's distributions (seeded).  Single key => one GPU."""
     from distributed_point_functions_amd import dpf as D
     from distributed_point_functions_amd import hip_abi as H
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("synthetic_* workloads evaluate one key on one GPU")
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
+        raise SystemExit("synthetic_* workloads evaluate one key on one GPU (--gpus 1)")
     H.load(require_gpu=True)
     mode = "direct" if args.workload == "synthetic_direct" else "hierarchical"
     device_ctx = args.workload == "synthetic_hierarchical_device"
@@ -870,7 +934,7 @@ def main_heavy_hitters(args):
     from distributed_point_functions_amd import hip_abi as H
     from distributed_point_functions_amd import sharding as S
 
-    world, rank, local, coll = init_ranks(torch, dist)
+    world, rank, local, coll = init_ranks(torch, dist, args.gpus)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -1002,7 +1066,7 @@ def main_dcf(args):
     from distributed_point_functions_amd import proto as pb
     from distributed_point_functions_amd import sharding as S
 
-    world, rank, local, coll = init_ranks(torch, dist)
+    world, rank, local, coll = init_ranks(torch, dist, args.gpus)
     H.load(require_gpu=True)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

@@ -64,3 +64,36 @@ def test_committed_profile_backs_the_headline(bench):
     tr = bench.profiled_traffic(bench.KERNEL, 1 << 30)
     assert tr is not None
     assert 8.5e9 < tr[0] < 30e9      # >= the 8 GiB written, well below HBM-bound
+
+
+def _run_bench(args, env_extra=None, timeout=120):
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
+                          env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_gpus_flag_never_falls_back_to_one_rank():
+    # No GPU here: `--gpus 2` without a launcher must refuse (exit non-zero)
+    # before it would start ranks, never run one rank and report n_gpus 1.
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "0"])
+    assert r.returncode != 0
+    assert "GPU(s) visible" in r.stderr and not r.stdout.strip()
+
+
+def test_gpus_flag_must_match_launcher_world_size():
+    r = _run_bench(["--gpus", "2"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+    r = _run_bench(["--gpus", "2", "--workload", "synthetic_direct"])
+    assert r.returncode != 0 and "one GPU" in r.stderr
+
+
+def test_launcher_cmd_relaunches_same_arguments(bench):
+    cmd = bench.launcher_cmd(["--gpus", "8", "--steps", "5"], 8, 29511)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29511"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "5"]
+    assert os.path.basename(cmd[-5]) == "bench.py"

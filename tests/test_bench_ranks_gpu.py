@@ -45,3 +45,31 @@ def test_two_ranks_on_one_gpu_weak_scaling_line():
     outputs = 2 * d["config"]["outputs_per_gpu"]
     assert d["value"] == pytest.approx(outputs / (d["ms_per_step"] * 1e-3), rel=1e-6)
     assert d["roofline"]["frac"] > 0
+
+
+def test_unlaunched_gpus_flag_starts_n_ranks():
+    # `python bench.py --gpus 2` with no launcher (the driver may call it that
+    # way): bench.py starts the two ranks itself and relays rank 0's line.
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(DPF_BENCH_ONE_GPU="1", PYTHONUNBUFFERED="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--no-cpu-baseline", "--log-domain", "26"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["process_group"]["world_size"] == 2
+    assert d["config"]["outputs_per_gpu"] == 1 << 26
+
+
+def test_unlaunched_gpus_beyond_visible_devices_fails():
+    import torch
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DPF_BENCH_ONE_GPU")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n),
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and not r.stdout.strip()
+    assert "visible" in r.stderr
