@@ -19,8 +19,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <unordered_map>
 
 #include "dpf/distributed_point_function.h"
@@ -44,9 +46,19 @@ using dpf_internal::U128Hash;
 namespace {
 // Host-phase timing of the batched path, printed at exit when
 // DPF_BATCH_HOST_TIMING is set (diagnostics for config 5a's host-bound levels).
+// Contexts on several threads add into it, so every update takes `mu`.
 struct HostTiming {
+  std::mutex mu;
   double t[6] = {0, 0, 0, 0, 0, 0};
   long calls = 0;
+  void add(int phase, double s) {
+    std::lock_guard<std::mutex> g(mu);
+    t[phase] += s;
+  }
+  void call() {
+    std::lock_guard<std::mutex> g(mu);
+    ++calls;
+  }
   ~HostTiming() {
     if (calls && std::getenv("DPF_BATCH_HOST_TIMING"))
       std::fprintf(stderr,
@@ -63,18 +75,62 @@ bool CacheOn() {
   const char* v = std::getenv("DPF_BATCH_NO_CACHE");
   return !(v && v[0] == '1');
 }
-// DPF_BATCH_CACHE_IN_PLACE=1 acts as if no spare cache buffer fitted (the
-// cache is rewritten in place): a test hook for that path.
-bool SpareOff() {
+// How a call that reads the expansion cache writes the next one.  Default:
+// into a spare buffer if one fits, else in place through a slot table, else
+// (no slot table possible) in place after gathering the start seeds.
+// DPF_BATCH_CACHE_MODE=spare|permute|gather forces one (a spare still only if
+// it fits; permute falls back to gather when no slot table exists), and
+// DPF_BATCH_CACHE_IN_PLACE=1 means gather: test and A/B hooks, read per call.
+enum class CacheMode { kAuto, kSpare, kPermute, kGather };
+CacheMode ForcedCacheMode() {
   const char* v = std::getenv("DPF_BATCH_CACHE_IN_PLACE");
-  return v && v[0] == '1';
+  if (v && v[0] == '1') return CacheMode::kGather;
+  const char* m = std::getenv("DPF_BATCH_CACHE_MODE");
+  if (!m) return CacheMode::kAuto;
+  const std::string s(m);
+  if (s == "spare") return CacheMode::kSpare;
+  if (s == "permute") return CacheMode::kPermute;
+  if (s == "gather") return CacheMode::kGather;
+  return CacheMode::kAuto;
+}
+
+// The slot table of an in-place rewrite (dpf_hip_eval_prefix_batch_cached_slots):
+// start node u = (tree index u >> s, sub-node) reads physical slot
+// start_slot[u >> s]; its 2^E leaves go to slot[(u << E) + l].  A slot read by
+// exactly one start node (s == 0) takes that node's leaf 0; every other leaf
+// takes the next slot no start node reads.  False if those run out.
+bool BuildSlotTable(const std::vector<int64_t>& start_slot, int64_t T, int s, int E,
+                    int64_t phys_stride, std::vector<int32_t>* slot) {
+  static thread_local std::vector<uint8_t> tl_read;
+  std::vector<uint8_t>& read = tl_read;
+  read.assign(static_cast<size_t>(phys_stride), 0);
+  for (int64_t i = 0; i < T; ++i) read[start_slot[i]] = 1;
+  const int64_t leaves = (T << s) << E;
+  slot->resize(static_cast<size_t>(leaves));
+  int64_t g = 0;  // next unread slot candidate
+  auto next_free = [&]() -> int64_t {
+    while (g < phys_stride && read[g]) ++g;
+    return g < phys_stride ? g++ : -1;
+  };
+  for (int64_t u = 0; u < (T << s); ++u) {
+    for (int64_t l = 0; l < (int64_t{1} << E); ++l) {
+      int64_t v;
+      if (l == 0 && s == 0) {
+        v = start_slot[u];
+      } else if ((v = next_free()) < 0) {
+        return false;
+      }
+      (*slot)[(u << E) + l] = static_cast<int32_t>(v);
+    }
+  }
+  return true;
 }
 struct PhaseClock {
   std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
   void mark(int phase) {
     if (!g_timing_on) return;
     auto now = std::chrono::steady_clock::now();
-    g_timing.t[phase] += std::chrono::duration<double>(now - last).count();
+    g_timing.add(phase, std::chrono::duration<double>(now - last).count());
     last = now;
   }
 };
@@ -145,6 +201,8 @@ void DeviceBatchContext::ReleaseExpansionCache() {
   Release(&leaf_seeds_, &leaf_seeds_cap_);
   Release(&leaf_spare_, &leaf_spare_cap_);
   Release(&slots_, &slots_cap_);
+  Release(&leaf_slot_, &leaf_slot_cap_);
+  leaf_phys_.clear();
   leaf_level_ = -1;
 }
 
@@ -161,7 +219,7 @@ void DeviceBatchContext::Reset(bool release_expansion_cache) {
 
 DeviceBatchContext::~DeviceBatchContext() {
   for (void* p : {seeds_, ctrl_, next_seeds_, next_ctrl_, parent_, path_, save_, offsets_,
-                  workspace_, stage_, stage2_, leaf_seeds_, leaf_spare_, slots_})
+                  workspace_, stage_, stage2_, leaf_seeds_, leaf_spare_, slots_, leaf_slot_})
     if (p) dpf_hip_free(p);
 }
 
@@ -232,7 +290,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         "Output size would be larger than 2**62. Please evaluate fewer hierarchy levels at once.");
 
   PhaseClock clk;
-  if (g_timing_on) ++g_timing.calls;
+  if (g_timing_on) g_timing.call();
   // Unique tree indices in first-seen order and each prefix's (tree index,
   // block index) (h:718-742).
   const int64_t P = static_cast<int64_t>(prefixes.size());
@@ -354,8 +412,27 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   // cache is rewritten in place; a failed allocation only turns the cache off.
   const int64_t leaf_stride = U << E;
   void* leaf_seeds = nullptr;
+  int64_t cache_stride = leaf_stride;  // physical row stride of the cache written
   bool swap_cache = false;
   bool gather = false;
+  bool permute = false;
+  // Physical cache slot of each tree index's node (cached calls).
+  static thread_local std::vector<int64_t> tl_start_slot;
+  std::vector<int64_t>& start_slot = tl_start_slot;
+  const uint128 leaf_mask = cached ? (uint128{1} << W1) - 1 : 0;  // W1 <= 62 when cached
+  if (cached) {
+    start_slot.resize(T);
+    const std::vector<int32_t>& phys = ctx.leaf_phys_;
+    dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i) {
+        const int64_t logical = (static_cast<int64_t>(from_root ? 0 : parent_of[i]) << W1) |
+                                static_cast<int64_t>(tree_indices[i] & leaf_mask);
+        start_slot[i] = phys.empty() ? logical : phys[logical];
+      }
+    });
+  }
+  static thread_local std::vector<int32_t> tl_leaf_slot;
+  std::vector<int32_t>& leaf_slot = tl_leaf_slot;
   // Headroom left on the device for everything else (the caller's buffers,
   // a second context): a quarter of it for the spare, an eighth for the cache.
   auto fits = [&](size_t bytes, size_t reserve_div) {
@@ -376,18 +453,25 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
       }
       leaf_seeds = ctx.leaf_seeds_;
     } else {
-      if (SpareOff()) {
-        // test hook: no spare
-      } else if (ctx.leaf_spare_cap_ < cache_need) {
+      const CacheMode mode = ForcedCacheMode();
+      const bool want_spare = mode == CacheMode::kAuto || mode == CacheMode::kSpare;
+      if (want_spare && ctx.leaf_spare_cap_ < cache_need) {
         // The spare may still be read by work in flight on the stream.
         HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
         ctx.Release(&ctx.leaf_spare_, &ctx.leaf_spare_cap_);
         if (!fits(cache_need, 4) || !ctx.TryAlloc(&ctx.leaf_spare_, &ctx.leaf_spare_cap_, cache_need))
           ++ctx.events_.spare_refused;
       }
-      if (ctx.leaf_spare_ && ctx.leaf_spare_cap_ >= cache_need && !SpareOff()) {
+      if (want_spare && ctx.leaf_spare_ && ctx.leaf_spare_cap_ >= cache_need) {
         leaf_seeds = ctx.leaf_spare_;
         swap_cache = true;
+      } else if (mode != CacheMode::kGather && leaf_stride <= ctx.leaf_stride_ &&
+                 BuildSlotTable(start_slot, T, s, E, ctx.leaf_stride_, &leaf_slot)) {
+        // In place through the slot table: no gather, no second buffer.
+        permute = true;
+        leaf_seeds = ctx.leaf_seeds_;
+        cache_stride = ctx.leaf_stride_;
+        ++ctx.events_.permuted;
       } else {
         gather = true;  // leaf_seeds is set once the gather is enqueued
         ++ctx.events_.in_place;
@@ -434,18 +518,11 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     path.resize(U);
   }
   const uint128 w1_mask = Wk >= 128 ? ~uint128{0} : ((uint128{1} << Wk) - 1);
-  const uint128 leaf_mask = cached ? (uint128{1} << W1) - 1 : 0;  // W1 <= 62 when cached
-  static thread_local std::vector<int64_t> tl_slots;
-  std::vector<int64_t>& slots = tl_slots;
-  if (gather) slots.resize(T);
   dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
       const uint128 low = tree_indices[i] & w1_mask;
-      // Cached: the cache slot of tree index i (its parent's leaf row).
-      const int64_t slot = cached ? (static_cast<int64_t>(from_root ? 0 : parent_of[i]) << W1) |
-                                        static_cast<int64_t>(tree_indices[i] & leaf_mask)
-                                  : 0;
-      if (gather) slots[i] = slot;
+      // Cached: the physical cache slot of tree index i.
+      const int64_t slot = cached ? start_slot[i] : 0;
       const int32_t start = direct ? static_cast<int32_t>(slot)
                             : gather ? static_cast<int32_t>(i)
                                      : (from_root ? 0 : parent_of[i]);
@@ -473,7 +550,8 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     // The start seeds (and, with update_ctx, the new partial evaluations),
     // read before the kernel rewrites the cache.
     DPF_RETURN_IF_ERROR(ensure(&ctx.slots_, &ctx.slots_cap_, T * sizeof(int64_t)));
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.slots_, slots.data(), T * sizeof(int64_t), stream));
+    HIP_RETURN_IF_ERROR(
+        dpf_hip_memcpy_h2d(ctx.slots_, start_slot.data(), T * sizeof(int64_t), stream));
     HIP_RETURN_IF_ERROR(dpf_hip_gather_seeds(
         K, T, static_cast<const int64_t*>(ctx.slots_), static_cast<const dpf_block*>(ctx.leaf_seeds_),
         ctx.leaf_stride_, static_cast<dpf_block*>(ctx.next_seeds_),
@@ -489,6 +567,12 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         ++ctx.events_.cache_refused;
     }
     leaf_seeds = ctx.leaf_seeds_;
+  }
+  if (permute) {
+    const size_t bytes = leaf_slot.size() * sizeof(int32_t);
+    DPF_RETURN_IF_ERROR(ensure(&ctx.leaf_slot_, &ctx.leaf_slot_cap_, bytes));
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.leaf_slot_, leaf_slot.data(), bytes, stream));
+    ctx.leaf_level_ = -1;  // rewritten in place by this call's kernel
   }
   std::vector<int64_t> offsets;
   if (!identity) {
@@ -514,14 +598,15 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
                                : gather ? T
                                         : static_cast<int64_t>(ctx.partial_prefixes_.size());
   auto launch = [&](int sum_mode, void* out, uint64_t* workspace) {
-    return FromHip(dpf_hip_eval_prefix_batch_cached(
+    return FromHip(dpf_hip_eval_prefix_batch_cached_slots(
         K, U, Wk + s, update_ctx && !gather ? Wk : -1, E, cached ? Dprev : start_level,
         keys.num_levels(), keys.seed(), keys.party(), start_seeds, start_ctrl, start_stride,
         static_cast<const int32_t*>(ctx.parent_), static_cast<const dpf_block*>(ctx.path_),
         static_cast<const int32_t*>(ctx.save_), static_cast<dpf_block*>(ctx.next_seeds_),
         static_cast<uint8_t*>(ctx.next_ctrl_), T, keys.cw_seed(), keys.cw_left(), keys.cw_right(),
         &kl, &kr, &kv, &desc, cepb, keys.value_correction(hierarchy_level), sum_mode, workspace,
-        out, static_cast<dpf_block*>(leaf_seeds), leaf_stride, stream));
+        out, static_cast<dpf_block*>(leaf_seeds), cache_stride,
+        permute ? static_cast<const int32_t*>(ctx.leaf_slot_) : nullptr, stream));
   };
   if (native_sum) {
     void* target = device_out;
@@ -568,7 +653,11 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   }
   ctx.leaf_level_ = leaf_seeds ? hierarchy_level : -1;
   ctx.leaf_de_ = dE;
-  ctx.leaf_stride_ = leaf_stride;
+  ctx.leaf_stride_ = cache_stride;
+  if (permute)
+    ctx.leaf_phys_.assign(leaf_slot.begin(), leaf_slot.end());
+  else
+    ctx.leaf_phys_.clear();   // written in leaf order
   // After the last level nothing reads the cache; its buffers stay allocated
   // for the next pass over the hierarchy (Reset()), because giving them back
   // and regrowing them level by level (4, 16, 64 GiB for 2^20 heavy-hitters

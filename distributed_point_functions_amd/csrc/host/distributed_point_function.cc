@@ -11,11 +11,13 @@
 #include <sys/random.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <mutex>
 #include <unordered_map>
 
 #include "dpf_hip.h"
@@ -822,10 +824,76 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
   return total;
 }
 
-StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
-    const DpfKey& key, int hierarchy_level, Span<const uint128> evaluation_points,
-    EvaluationContext* ctx, const ValueType* requested_type) const {
+namespace {
+// Host-phase timing of EvaluateAt, printed at exit when DPF_HOST_TIMING is
+// set (the first 10 calls, allocations and page-locked buffers, not counted):
+// checks = the fused domain check + path / block-index pass over the points,
+// key = key validation, value correction, context lookups and correction
+// words, upload = the one packed H2D, launch = the point kernel's launch,
+// copy = waiting for the kernel + the D2H into the caller's vector (unpacked
+// chunk by chunk).
+struct AtTiming {
+  double t[5] = {0, 0, 0, 0, 0};
+  long calls = 0;
+  ~AtTiming() {
+    const double n = static_cast<double>(calls - 10);
+    if (calls > 10 && std::getenv("DPF_HOST_TIMING"))
+      std::fprintf(stderr,
+                   "[EvaluateAt host timing] calls=%ld per call: checks=%.2fus key=%.2fus "
+                   "upload=%.2fus launch=%.2fus copy=%.2fus\n",
+                   calls, t[0] * 1e6 / n, t[1] * 1e6 / n, t[2] * 1e6 / n, t[3] * 1e6 / n,
+                   t[4] * 1e6 / n);
+  }
+};
+AtTiming g_at_timing;
+std::mutex g_at_timing_mu;
+struct AtClock {
+  std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+  AtClock() {
+    if (!g_until_timing_on) return;
+    std::lock_guard<std::mutex> lock(g_at_timing_mu);
+    ++g_at_timing.calls;
+  }
+  void mark(int phase) {
+    if (!g_until_timing_on) return;
+    auto now = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> lock(g_at_timing_mu);
+    if (g_at_timing.calls > 10)
+      g_at_timing.t[phase] += std::chrono::duration<double>(now - last).count();
+    last = now;
+  }
+};
+
+// First index in [0, n) whose point exceeds max_point (n if none), found on
+// host threads while `fill(lo, hi)` writes the kernel's per-point arrays.
+template <typename Fill>
+int64_t CheckAndFillPoints(Span<const uint128> points, uint128 max_point, Fill fill) {
+  const int64_t n = static_cast<int64_t>(points.size());
+  std::atomic<int64_t> bad{n};
+  dpf_internal::ParallelFor(
+      n,
+      [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i)
+          if (points[i] > max_point) {
+            int64_t cur = bad.load();
+            while (i < cur && !bad.compare_exchange_weak(cur, i)) {
+            }
+            return;
+          }
+        fill(lo, hi);
+      },
+      int64_t{1} << 16);
+  return bad.load();
+}
+}  // namespace
+
+Status DistributedPointFunction::EvaluateAtToHost(const DpfKey& key, int hierarchy_level,
+                                                  Span<const uint128> evaluation_points,
+                                                  EvaluationContext* ctx,
+                                                  const ValueType* requested_type,
+                                                  const HostSink& sink) const {
   // h:839-1010
+  AtClock clk;
   if (ctx != nullptr && &key != &ctx->key())
     return InvalidArgumentError("`key` and `ctx->key()` must refer to the same object");
   if (hierarchy_level < 0) return InvalidArgumentError("`hierarchy_level` must be non-negative");
@@ -842,54 +910,66 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
   const int log_domain_size = parameters()[hierarchy_level].log_domain_size();
   const uint128 max_point =
       log_domain_size < 128 ? (static_cast<uint128>(1) << log_domain_size) - 1 : Uint128Max();
-  for (int64_t i = 0; i < n; ++i)
-    if (evaluation_points[i] > max_point)
-      return InvalidArgumentError("`evaluation_points[" + std::to_string(i) +
-                                  "]` larger than the domain size at hierarchy level " +
-                                  std::to_string(hierarchy_level));
-  DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
-  if (n == 0) return std::vector<uint8_t>{};
-  DPF_ASSIGN_OR_RETURN(std::vector<uint128> vcw, ValueCorrectionLeaves(key, hierarchy_level));
   const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
   const int E = f.elements_per_block;
-  const int bib = log_domain_size - hierarchy_to_tree()[hierarchy_level];
-  std::vector<uint128> tree_indices(evaluation_points.begin(), evaluation_points.end());
-  std::vector<int32_t> block_index(n, 0);
-  if (E > 1) {
-    for (int64_t i = 0; i < n; ++i) {
-      tree_indices[i] = evaluation_points[i] >> bib;
-      block_index[i] = static_cast<int32_t>(evaluation_points[i] & ((static_cast<uint128>(1) << bib) - 1));
-    }
-  }
+  const int stop_level = hierarchy_to_tree()[hierarchy_level];
+  const int bib = log_domain_size - stop_level;
+  const int start_level = ctx ? stop_level : 0;
+  const int L = stop_level - start_level;
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
-  const int stop_level = hierarchy_to_tree()[hierarchy_level];
-  int start_level = 0;
+  PackedUploads& up = s->packed;
+  DPF_RETURN_IF_ERROR(up.Reset());
+  // The domain check (h:861-874), tree indices and block indices (h:907-925)
+  // in ONE pass on host threads, written straight into the page-locked
+  // upload image.
+  const size_t nvcw = static_cast<size_t>(E) * f.leaves.size();
+  up.Prepare(7 * 256 + static_cast<size_t>(n) * (sizeof(dpf_block) + sizeof(int32_t)) +
+             static_cast<size_t>(L + 1) * (sizeof(dpf_block) + 2) + nvcw * sizeof(dpf_block) + 32);
+  size_t o_paths, o_bi;
+  dpf_block* paths = up.Reserve<dpf_block>(n, &o_paths);
+  int32_t* block_index = up.Reserve<int32_t>(n, &o_bi);
+  const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
+  const int64_t bad = CheckAndFillPoints(evaluation_points, max_point, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      const uint128 x = evaluation_points[i];
+      paths[i] = ToBlock(E > 1 ? x >> bib : x);
+      block_index[i] = E > 1 ? static_cast<int32_t>(x & bmask) : 0;
+    }
+  });
+  if (bad < n)
+    return InvalidArgumentError("`evaluation_points[" + std::to_string(bad) +
+                                "]` larger than the domain size at hierarchy level " +
+                                std::to_string(hierarchy_level));
+  clk.mark(0);
+  DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
+  if (n == 0) {
+    (void)sink.reserve(0);
+    return OkStatus();
+  }
+  DPF_ASSIGN_OR_RETURN(std::vector<uint128> vcw, ValueCorrectionLeaves(key, hierarchy_level));
   DeviceStart start;
   if (ctx) {
-    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(MakeConstSpan(tree_indices), hierarchy_level,
+    // The tree indices, as uint128 memory images (paths is 256-byte aligned).
+    const Span<const uint128> tree_indices(reinterpret_cast<const uint128*>(paths),
+                                           static_cast<size_t>(n));
+    DPF_RETURN_IF_ERROR(ComputePartialEvaluations(tree_indices, hierarchy_level,
                                                   /*update_ctx=*/true, *ctx, &start, nullptr,
                                                   nullptr));
-    start_level = stop_level;
   }
-  // All argument arrays in one packed upload (PackedUploads).
-  std::vector<dpf_block> paths(n);
-  for (int64_t i = 0; i < n; ++i) paths[i] = ToBlock(tree_indices[i]);
-  const int L = stop_level - start_level;
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
   const dpf_block root = ToBlock(FromProtoBlock(key.seed()));
   const uint8_t party = static_cast<uint8_t>(key.party() & 1);
-  PackedUploads& up = s->packed;
-  DPF_RETURN_IF_ERROR(up.Reset());
-  const size_t o_paths = up.Add(paths.data(), paths.size());
-  const size_t o_bi = up.Add(block_index.data(), block_index.size());
   const PackedCws o_cw = AddCorrectionWords(key, start_level, stop_level, up);
   const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());
   const size_t o_root = up.Add(&root, 1);
   const size_t o_party = up.Add(&party, 1);
+  clk.mark(1);
   DPF_RETURN_IF_ERROR(up.Commit(nullptr));
-  DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
+  const size_t bytes = static_cast<size_t>(n) * f.packed_size;
+  DPF_RETURN_IF_ERROR(s->out.Reserve(bytes));
+  clk.mark(2);
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   HIP_RETURN_IF_ERROR(dpf_hip_eval_points(
@@ -899,10 +979,23 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
       up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), s->out.get(),
       nullptr));
   DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
-  std::vector<uint8_t> out;
-  HIP_RETURN_IF_ERROR(CopyToHostVector(&out, s->out.get(),
-                                       static_cast<size_t>(n) * f.packed_size, nullptr));
+  clk.mark(3);
+  // Packed elements straight into the caller's result (h:983-1003 outputs):
+  // integers copied, tuples / IntModN / XorWrapper unpacked chunk by chunk out
+  // of the page-locked staging buffers.
+  HIP_RETURN_IF_ERROR(dpf_internal::CopyToHostSink(sink, sink.reserve(bytes), s->out.get(), bytes,
+                                                   nullptr));
+  clk.mark(4);
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
+  return OkStatus();
+}
+
+StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtPacked(
+    const DpfKey& key, int hierarchy_level, Span<const uint128> evaluation_points,
+    EvaluationContext* ctx, const ValueType* requested_type) const {
+  std::vector<uint8_t> out;
+  DPF_RETURN_IF_ERROR(EvaluateAtToHost(key, hierarchy_level, evaluation_points, ctx,
+                                       requested_type, dpf_internal::VectorSink(&out)));
   return out;
 }
 

@@ -464,6 +464,7 @@ PYBIND11_MODULE(_dpf_host, m) {
         d["cache_refused"] = e.cache_refused;
         d["spare_refused"] = e.spare_refused;
         d["in_place"] = e.in_place;
+        d["permuted"] = e.permuted;
         d["evicted_spare"] = e.evicted_spare;
         d["evicted_cache"] = e.evicted_cache;
         d["alloc_failures"] = e.alloc_failures;

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -345,12 +346,16 @@ class HostStaging {
   std::vector<void*> free_events_;
 };
 
-// The small argument arrays of ONE call packed into one image and copied with
-// a single asynchronous H2D (a call's 6-8 separate copies cost ~5 us of API
-// time each).  Usage: Reset(); off = Add(data, n) per array; Commit(stream);
-// then Ptr<T>(off) are the device addresses, valid until the next Reset().
-// Reset() waits for the previous call's stream, so neither the page-locked
-// image nor the device arena is rewritten while a copy or kernel still reads it.
+// The argument arrays of ONE call packed into one image and copied with a
+// single asynchronous H2D (a call's 6-8 separate copies cost ~5 us of API
+// time each).  The image is built straight in page-locked memory (no second
+// host pass over it before the DMA; callers may also fill an array in place:
+// Reserve).  Usage: Reset(); [Prepare(total bytes)]; off = Add(data, n) or
+// p = Reserve<T>(n, &off) per array; Commit(stream); then Ptr<T>(off) are the
+// device addresses, valid until the next Reset().  Reset() waits for the
+// previous call's stream, so neither the page-locked image nor the device
+// arena is rewritten while a copy or kernel still reads it.  Images above
+// kMaxPinned are built in pageable memory and copied synchronously.
 class PackedUploads {
  public:
   PackedUploads() = default;
@@ -366,9 +371,13 @@ class PackedUploads {
   Status Reset() {
     if (pending_) HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
     pending_ = false;
-    image_.clear();
+    size_ = 0;
+    pageable_ = false;
     return OkStatus();
   }
+  // Room for `bytes` of arrays (each array 256-byte aligned): pointers from
+  // Reserve stay valid until Commit only when the image never has to grow.
+  void Prepare(size_t bytes) { Grow(bytes); }
   // Records that the work queued on `stream` so far reads the arena.
   Status MarkUsed(void* stream) {
     if (!event_) HIP_RETURN_IF_ERROR(dpf_hip_event_create(&event_));
@@ -376,31 +385,31 @@ class PackedUploads {
     pending_ = true;
     return OkStatus();
   }
+  // Space for `count` elements of T in the image, to be filled by the caller
+  // (valid until the image grows: Prepare first).
+  template <typename T>
+  T* Reserve(size_t count, size_t* off) {
+    *off = (size_ + 255) & ~size_t{255};
+    const size_t end = *off + std::max<size_t>(count * sizeof(T), 1);
+    Grow(end);
+    size_ = end;
+    return reinterpret_cast<T*>(base() + *off);
+  }
   template <typename T>
   size_t Add(const T* data, size_t count) {
-    const size_t off = (image_.size() + 255) & ~size_t{255};
-    image_.resize(off + std::max<size_t>(count * sizeof(T), 1));
-    if (count) std::memcpy(image_.data() + off, data, count * sizeof(T));
+    size_t off;
+    T* p = Reserve<T>(count, &off);
+    if (count) std::memcpy(p, data, count * sizeof(T));
     return off;
   }
   Status Commit(void* stream) {
-    const size_t bytes = image_.size();
-    if (bytes == 0) return OkStatus();
-    if (bytes > kMaxPinned) {  // large batches: bounce-buffered synchronous copy
-      DPF_RETURN_IF_ERROR(arena_.Reserve(bytes));
-      return FromHip(dpf_hip_memcpy_h2d(arena_.get(), image_.data(), bytes, stream));
-    }
-    if (bytes > cap_) {
-      if (pinned_) dpf_hip_host_free(pinned_);
-      pinned_ = nullptr;
-      cap_ = 0;
-      const size_t want = std::max<size_t>(bytes, size_t{1} << 20);
-      HIP_RETURN_IF_ERROR(dpf_hip_host_alloc(&pinned_, want));
-      cap_ = want;
+    if (size_ == 0) return OkStatus();
+    if (pageable_) {  // large batches: a synchronous copy from pageable memory
+      DPF_RETURN_IF_ERROR(arena_.Reserve(size_));
+      return FromHip(dpf_hip_memcpy_h2d(arena_.get(), image_.get(), size_, stream));
     }
     DPF_RETURN_IF_ERROR(arena_.Reserve(cap_));
-    std::memcpy(pinned_, image_.data(), bytes);
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(arena_.get(), pinned_, bytes, stream));
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(arena_.get(), pinned_, size_, stream));
     return MarkUsed(stream);
   }
   template <typename T>
@@ -409,8 +418,44 @@ class PackedUploads {
   }
 
  private:
-  static constexpr size_t kMaxPinned = size_t{16} << 20;
-  std::vector<uint8_t> image_;
+  static constexpr size_t kMaxPinned = size_t{64} << 20;
+  char* base() { return pageable_ ? image_.get() : static_cast<char*>(pinned_); }
+  // Pageable image of at least `end` bytes holding [0, size_) of the current one
+  // (uninitialised beyond: no value-initialisation pass over a large image).
+  void GrowPageable(size_t end, const char* from) {
+    if (image_ && image_cap_ >= end) {
+      if (from != image_.get() && size_) std::memcpy(image_.get(), from, size_);
+      return;
+    }
+    std::unique_ptr<char[]> ni(new char[end]);
+    if (size_) std::memcpy(ni.get(), from, size_);
+    image_ = std::move(ni);
+    image_cap_ = end;
+  }
+  // Makes [0, end) of the image addressable, keeping [0, size_).
+  void Grow(size_t end) {
+    if (pageable_) {
+      if (end > image_cap_) GrowPageable(std::max(end, image_cap_ + image_cap_ / 2), image_.get());
+      return;
+    }
+    if (end <= cap_) return;
+    void* np = nullptr;
+    const size_t want = std::max<size_t>({end, cap_ + cap_ / 2, size_t{1} << 20});
+    if (end > kMaxPinned || dpf_hip_host_alloc(&np, want) != 0) {
+      // Too large to keep page-locked (or no page-locked memory): pageable.
+      GrowPageable(end, static_cast<const char*>(pinned_));
+      pageable_ = true;
+      return;
+    }
+    if (size_) std::memcpy(np, pinned_, size_);
+    if (pinned_) dpf_hip_host_free(pinned_);
+    pinned_ = np;
+    cap_ = want;
+  }
+  std::unique_ptr<char[]> image_;  // pageable image (pageable_)
+  size_t image_cap_ = 0;
+  size_t size_ = 0;
+  bool pageable_ = false;
   void* pinned_ = nullptr;
   size_t cap_ = 0;
   DeviceBuffer arena_;

@@ -38,6 +38,21 @@
 #else
 #define DPF_ROUND_LOOP _Pragma("unroll 1")
 #endif
+// Rounds 1..DPF_L1_ROUNDS read their T-table entries through the vector L1
+// (lk.l1: one 1 KiB T0 table in global memory, rotated per table) instead of
+// LDS, so the two lookup engines work side by side (an
+// A/B variant, 0 = every round from LDS).
+#ifndef DPF_L1_ROUNDS
+#define DPF_L1_ROUNDS 0
+#endif
+#ifndef DPF_L1_AB
+#define DPF_L1_AB 1   // 0: the ILP-N chains (encryptAB) keep every round in LDS
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && DPF_L1_ROUNDS > 0
+#define DPF_L1_FIRST (1 + DPF_L1_ROUNDS)
+#else
+#define DPF_L1_FIRST 1
+#endif
 
 namespace dpf_aes {
 
@@ -102,10 +117,25 @@ DPF_HD Block4 sigma(Block4 x) { return Block4{x.w2, x.w3, x.w2 ^ x.w0, x.w3 ^ x.
 template <class LK, class RK>
 DPF_HD Block4 encrypt(Block4 s, const LK& lk, const RK& rk) {
   uint32_t w0 = s.w0 ^ rk(0), w1 = s.w1 ^ rk(1), w2 = s.w2 ^ rk(2), w3 = s.w3 ^ rk(3);
+#if DPF_L1_FIRST > 1
+  DPF_UNROLL
+  for (int r = 1; r < DPF_L1_FIRST; ++r) {
+    uint32_t n0 = lk.xor3(lk.template l1<0, 0>(w0), lk.template l1<1, 1>(w1), lk.template l1<2, 2>(w2));
+    uint32_t n1 = lk.xor3(lk.template l1<0, 0>(w1), lk.template l1<1, 1>(w2), lk.template l1<2, 2>(w3));
+    uint32_t n2 = lk.xor3(lk.template l1<0, 0>(w2), lk.template l1<1, 1>(w3), lk.template l1<2, 2>(w0));
+    uint32_t n3 = lk.xor3(lk.template l1<0, 0>(w3), lk.template l1<1, 1>(w0), lk.template l1<2, 2>(w1));
+    n0 = rk.mix(lk, n0, lk.template l1<3, 3>(w3), 4 * r + 0);
+    n1 = rk.mix(lk, n1, lk.template l1<3, 3>(w0), 4 * r + 1);
+    n2 = rk.mix(lk, n2, lk.template l1<3, 3>(w1), 4 * r + 2);
+    n3 = rk.mix(lk, n3, lk.template l1<3, 3>(w2), 4 * r + 3);
+    w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+  }
+  __builtin_amdgcn_sched_barrier(0);  // hipcc's iterative-ilp RA crashes without it
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   DPF_ROUND_LOOP
 #endif
-  for (int r = 1; r < 10; ++r) {
+  for (int r = DPF_L1_FIRST; r < 10; ++r) {
     uint32_t n0 = lk.xor3(lk.template lookup<0, 0>(w0), lk.template lookup<1, 1>(w1),
                           lk.template lookup<2, 2>(w2));
     uint32_t n1 = lk.xor3(lk.template lookup<0, 0>(w1), lk.template lookup<1, 1>(w2),
@@ -151,10 +181,34 @@ template <class LK, class RKA, class RKB>
 DPF_HD void encrypt2(Block4& sa, Block4& sb, const LK& lk, const RKA& ra, const RKB& rb) {
   uint32_t a0 = sa.w0 ^ ra(0), a1 = sa.w1 ^ ra(1), a2 = sa.w2 ^ ra(2), a3 = sa.w3 ^ ra(3);
   uint32_t b0 = sb.w0 ^ rb(0), b1 = sb.w1 ^ rb(1), b2 = sb.w2 ^ rb(2), b3 = sb.w3 ^ rb(3);
+#if DPF_L1_FIRST > 1
+  DPF_UNROLL
+  for (int r = 1; r < DPF_L1_FIRST; ++r) {
+    uint32_t n0 = lk.xor3(lk.template l1<0, 0>(a0), lk.template l1<1, 1>(a1), lk.template l1<2, 2>(a2));
+    uint32_t n1 = lk.xor3(lk.template l1<0, 0>(a1), lk.template l1<1, 1>(a2), lk.template l1<2, 2>(a3));
+    uint32_t n2 = lk.xor3(lk.template l1<0, 0>(a2), lk.template l1<1, 1>(a3), lk.template l1<2, 2>(a0));
+    uint32_t n3 = lk.xor3(lk.template l1<0, 0>(a3), lk.template l1<1, 1>(a0), lk.template l1<2, 2>(a1));
+    uint32_t m0 = lk.xor3(lk.template l1<0, 0>(b0), lk.template l1<1, 1>(b1), lk.template l1<2, 2>(b2));
+    uint32_t m1 = lk.xor3(lk.template l1<0, 0>(b1), lk.template l1<1, 1>(b2), lk.template l1<2, 2>(b3));
+    uint32_t m2 = lk.xor3(lk.template l1<0, 0>(b2), lk.template l1<1, 1>(b3), lk.template l1<2, 2>(b0));
+    uint32_t m3 = lk.xor3(lk.template l1<0, 0>(b3), lk.template l1<1, 1>(b0), lk.template l1<2, 2>(b1));
+    n0 = ra.mix(lk, n0, lk.template l1<3, 3>(a3), 4 * r + 0);
+    n1 = ra.mix(lk, n1, lk.template l1<3, 3>(a0), 4 * r + 1);
+    n2 = ra.mix(lk, n2, lk.template l1<3, 3>(a1), 4 * r + 2);
+    n3 = ra.mix(lk, n3, lk.template l1<3, 3>(a2), 4 * r + 3);
+    m0 = rb.mix(lk, m0, lk.template l1<3, 3>(b3), 4 * r + 0);
+    m1 = rb.mix(lk, m1, lk.template l1<3, 3>(b0), 4 * r + 1);
+    m2 = rb.mix(lk, m2, lk.template l1<3, 3>(b1), 4 * r + 2);
+    m3 = rb.mix(lk, m3, lk.template l1<3, 3>(b2), 4 * r + 3);
+    a0 = n0; a1 = n1; a2 = n2; a3 = n3;
+    b0 = m0; b1 = m1; b2 = m2; b3 = m3;
+  }
+  __builtin_amdgcn_sched_barrier(0);  // hipcc's iterative-ilp RA crashes without it
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   DPF_ROUND_LOOP
 #endif
-  for (int r = 1; r < 10; ++r) {
+  for (int r = DPF_L1_FIRST; r < 10; ++r) {
     uint32_t n0 = lk.xor3(lk.template lookup<0, 0>(a0), lk.template lookup<1, 1>(a1),
                           lk.template lookup<2, 2>(a2));
     uint32_t n1 = lk.xor3(lk.template lookup<0, 0>(a1), lk.template lookup<1, 1>(a2),
@@ -224,10 +278,30 @@ DPF_UNROLL
     w[i][2] = st[i].w2 ^ key(i, 2);
     w[i][3] = st[i].w3 ^ key(i, 3);
   }
+#if DPF_L1_FIRST > 1 && DPF_L1_AB
+  DPF_UNROLL
+  for (int r = 1; r < DPF_L1_FIRST; ++r) {
+    // Two chains at a time (a scheduling region each): the whole ILP-N round
+    // at once crashes hipcc's register allocator under iterative-ilp.
+DPF_UNROLL
+    for (int i = 0; i < N; ++i) {
+      uint32_t n[4];
+DPF_UNROLL
+      for (int c = 0; c < 4; ++c)
+        n[c] = mix(i, lk.xor3(lk.template l1<0, 0>(w[i][c]), lk.template l1<1, 1>(w[i][(c + 1) & 3]),
+                              lk.template l1<2, 2>(w[i][(c + 2) & 3])),
+                   lk.template l1<3, 3>(w[i][(c + 3) & 3]), 4 * r + c);
+DPF_UNROLL
+      for (int c = 0; c < 4; ++c) w[i][c] = n[c];
+      if (i % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // hipcc's iterative-ilp RA crashes without it
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
   DPF_ROUND_LOOP
 #endif
-  for (int r = 1; r < 10; ++r) {
+  for (int r = DPF_L1_AB ? DPF_L1_FIRST : 1; r < 10; ++r) {
     uint32_t n[N][4];
 DPF_UNROLL
     for (int i = 0; i < N; ++i) {
@@ -311,6 +385,8 @@ struct HostLookup {
   }
   template <int T, int K>
   uint32_t lookup(uint32_t w) const { return t[T][(w >> (8 * K)) & 0xff]; }
+  template <int T, int K>
+  uint32_t l1(uint32_t w) const { return lookup<T, K>(w); }
   uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) const { return a ^ b ^ c; }
 };
 

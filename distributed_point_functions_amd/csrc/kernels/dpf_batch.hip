@@ -88,6 +88,7 @@ struct BatchLevelParams {
   // 323-343), so the cache keeps the control bit there: one 16-byte store.
   dpf_block* leaf_seeds;
   int64_t leaf_stride;
+  const int32_t* leaf_slot;   // NULL: leaf l of start node u at slot (u << E) + l
   RoundKeys rkl, rkr, rkd, rkv;
 };
 
@@ -98,12 +99,12 @@ __device__ __forceinline__ uint4 cw_block(const dpf_block* p) {
 }
 
 // Two path steps of two different keys (own correction words), interleaved.
-__device__ __forceinline__ void path_step2k(const LdsLookup& lk, const RoundKeys& rkl,
-                                            const RoundKeys& rkd, Block4& s0, uint32_t& t0,
+__device__ __forceinline__ void path_step2k(const LdsLookup& lk, KeyRef rkl,
+                                            KeyRef rkd, Block4& s0, uint32_t& t0,
                                             uint4 cs0, uint32_t cc0, Block4& s1, uint32_t& t1,
                                             uint4 cs1, uint32_t cc1, uint32_t bit) {
   Block4 h0 = s0, h1 = s1;
-  const SelectRK rk{rkl.k, rkd.k, 0u - bit};
+  const SelectRK rk{rkl, rkd, 0u - bit};
   dpf_aes::mmo_hash2(h0, h1, lk, rk, rk);
   uint32_t m0 = 0u - t0, m1 = 0u - t1;
   h0.w0 ^= cs0.x & m0; h0.w1 ^= cs0.y & m0; h0.w2 ^= cs0.z & m0; h0.w3 ^= cs0.w & m0;
@@ -162,13 +163,13 @@ struct FastV {
   __device__ __forceinline__ void pair(const LdsLookup& lk, const BatchLevelParams& p, Block4 s0,
                                        uint32_t t0, Block4 s1, uint32_t t1, Val& v0,
                                        Val& v1) const {
-    dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+    dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{lk.ks.v}, UniformRK{lk.ks.v});
     v0 = correct(s0, t0);
     v1 = correct(s1, t1);
   }
   __device__ __forceinline__ void one(const LdsLookup& lk, const BatchLevelParams& p, Block4 s,
                                       uint32_t t, Val& v) const {
-    v = correct(dpf_aes::mmo_hash(s, lk, UniformRK{p.rkv.k}), t);
+    v = correct(dpf_aes::mmo_hash(s, lk, UniformRK{lk.ks.v}), t);
   }
   __device__ __forceinline__ static void zero(Val& a) { a = Block4{0, 0, 0, 0}; }
   __device__ __forceinline__ void acc_add(Val& a, const Val& v) const {
@@ -259,8 +260,8 @@ struct Mod32V {
     if (ILP4 && b == 2) {
       // Both leaves' two blocks as one interleaved quadruple.
       Block4 h[4] = {s0, add_small(s0, 1u), s1, add_small(s1, 1u)};
-      const UniformRK rk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
-                               UniformRK{p.rkv.k}};
+      const UniformRK rk[4] = {UniformRK{lk.ks.v}, UniformRK{lk.ks.v}, UniformRK{lk.ks.v},
+                               UniformRK{lk.ks.v}};
       dpf_aes::mmo_hashN<4>(h, lk, rk);
       w0[0] = h[0].w0; w0[1] = h[0].w1; w0[2] = h[0].w2; w0[3] = h[0].w3;
       w0[4] = h[1].w0; w0[5] = h[1].w1; w0[6] = h[1].w2; w0[7] = h[1].w3;
@@ -271,7 +272,7 @@ struct Mod32V {
       for (int j = 0; j < 2; ++j) {
         if (j < b) {
           Block4 h0 = add_small(s0, (uint32_t)j), h1 = add_small(s1, (uint32_t)j);
-          dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+          dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{lk.ks.v}, UniformRK{lk.ks.v});
           w0[4 * j] = h0.w0; w0[4 * j + 1] = h0.w1; w0[4 * j + 2] = h0.w2; w0[4 * j + 3] = h0.w3;
           w1[4 * j] = h1.w0; w1[4 * j + 1] = h1.w1; w1[4 * j + 2] = h1.w2; w1[4 * j + 3] = h1.w3;
         } else {
@@ -288,11 +289,11 @@ struct Mod32V {
     uint32_t w[8];
     if (b == 2) {
       Block4 h0 = s, h1 = add_small(s, 1u);
-      dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+      dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{lk.ks.v}, UniformRK{lk.ks.v});
       w[0] = h0.w0; w[1] = h0.w1; w[2] = h0.w2; w[3] = h0.w3;
       w[4] = h1.w0; w[5] = h1.w1; w[6] = h1.w2; w[7] = h1.w3;
     } else {
-      Block4 h0 = dpf_aes::mmo_hash(s, lk, UniformRK{p.rkv.k});
+      Block4 h0 = dpf_aes::mmo_hash(s, lk, UniformRK{lk.ks.v});
       w[0] = h0.w0; w[1] = h0.w1; w[2] = h0.w2; w[3] = h0.w3;
       w[4] = w[5] = w[6] = w[7] = 0;
     }
@@ -352,7 +353,7 @@ struct GenericV {
   __device__ __forceinline__ void flush(const BatchLevelParams&, int64_t, const Val&) const {}
   __device__ __forceinline__ void store(const LdsLookup& lk, const BatchLevelParams& p, char* o,
                                         const Val& v) const {
-    g.convert_store(lk, p.rkv.k, v.s, v.t, 0, p.epl, o);
+    g.convert_store(lk, lk.ks.v, v.s, v.t, 0, p.epl, o);
   }
 };
 
@@ -364,7 +365,8 @@ struct GenericV {
 template <int MAXE, class V, class Sink>
 __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const BatchLevelParams& p,
                                                    const V& v, int64_t k, Block4 node,
-                                                   uint32_t t, int64_t leaf_at, Sink&& sink) {
+                                                   uint32_t t, int64_t leaf_row,
+                                                   int64_t leaf_first, Sink&& sink) {
   Block4 N[1 << MAXE];
   uint32_t T = 0;  // bit i = control bit of N[i]
   N[0] = node;
@@ -381,7 +383,7 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
       if (d == 0) {
         Block4 c0, c1;
         uint32_t t0, t1;
-        children_step(lk, p.rkl.k, p.rkr.k, N[0], T & 1u, cs, cc, c0, t0, c1, t1);
+        children_step(lk, lk.ks.l, lk.ks.r, N[0], T & 1u, cs, cc, c0, t0, c1, t1);
         N[0] = c0;
         N[1] = c1;
         T = t0 | (t1 << 1);
@@ -392,7 +394,7 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
         for (int i = (1 << d) - 1; i >= 1; i -= 2) {
           Block4 c[4];
           uint32_t t[4];
-          children_step_x2(lk, p.rkl.k, p.rkr.k, N[i], (T >> i) & 1u, N[i - 1], (T >> (i - 1)) & 1u,
+          children_step_x2(lk, lk.ks.l, lk.ks.r, N[i], (T >> i) & 1u, N[i - 1], (T >> (i - 1)) & 1u,
                            cs, cc, c, t);
           N[2 * i] = c[0];
           N[2 * i + 1] = c[1];
@@ -406,13 +408,16 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
   }
   // The expansion cache: this start node's 2^E leaves (node and control bit),
   // 2^E consecutive entries per lane.
-  if (leaf_at >= 0) {
+  // With a slot table (the cache rewritten in place, permuted) leaf i goes
+  // to its own slot; this thread has already read every cache entry it reads.
+  if (leaf_row >= 0) {
 #pragma unroll
     for (int i = 0; i < (1 << MAXE); ++i) {
       if (i < (1 << E)) {
         Block4 c = N[i];
         c.w0 |= (T >> i) & 1u;
-        store_block(p.leaf_seeds + leaf_at + i, c);
+        const int64_t slot = p.leaf_slot ? p.leaf_slot[leaf_first + i] : leaf_first + i;
+        store_block(p.leaf_seeds + leaf_row + slot, c);
       }
     }
   }
@@ -439,7 +444,8 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(
+      lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
   const int64_t U = p.num_starts;
   const int W = p.walk_levels;
   const int NL = 1 << p.expand_levels;
@@ -503,7 +509,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
         const uint32_t bit = path_bit(path, W - 1 - j);
         const uint32_t cca = (uint32_t)(la[j] & 1) | ((uint32_t)(ra[j] & 1) << 1);
         const uint32_t ccb = (uint32_t)(lb[j] & 1) | ((uint32_t)(rb[j] & 1) << 1);
-        path_step2k(lk, p.rkl, p.rkd, sa, ta, cw_block(ca + j), cca, sb, tb, cw_block(cb + j), ccb,
+        path_step2k(lk, lk.ks.l, lk.ks.d, sa, ta, cw_block(ca + j), cca, sb, tb, cw_block(cb + j), ccb,
                     bit);
       }
       // 2.-4. expansion, conversion and sum/store, one key at a time.
@@ -514,10 +520,10 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
         vk.key(p, k);
         const Block4 node = which ? sb : sa;
         const uint32_t tn = which ? tb : ta;
-        const int64_t leaf_at =
-            p.leaf_seeds && valid ? k * p.leaf_stride + (u << p.expand_levels) : -1;
+        const int64_t leaf_row = p.leaf_seeds && valid ? k * p.leaf_stride : -1;
+        const int64_t leaf_first = u << p.expand_levels;
         if constexpr (SUM) {
-          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_at,
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_row, leaf_first,
                                    [&](int l, const typename V::Val& val) {
 #pragma unroll
             for (int i = 0; i < (1 << MAXE); ++i)
@@ -525,7 +531,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
           });
         } else {
           char* row = p.out + k * p.out_row + (u << p.expand_levels) * (int64_t)p.epl * p.esz;
-          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_at,
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_row, leaf_first,
                                    [&](int l, const typename V::Val& val) {
             if (valid) vk.store(lk, p, row + (int64_t)l * p.epl * p.esz, val);
           });
@@ -718,6 +724,24 @@ int dpf_hip_eval_prefix_batch_cached(
     const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
     const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
     dpf_block* leaf_cache, int64_t leaf_stride, void* stream) {
+  return dpf_hip_eval_prefix_batch_cached_slots(
+      num_keys, num_starts, walk_levels, save_after, expand_levels, cw_first, cw_stride, key_seed,
+      party, seeds_in, control_in, in_stride, parent, path, save_index, seeds_out, control_out,
+      out_stride, cw_seed, cw_left, cw_right, key_left, key_right, key_value, desc,
+      elements_per_leaf, value_correction, sum, workspace, out, leaf_cache, leaf_stride, nullptr,
+      stream);
+}
+
+int dpf_hip_eval_prefix_batch_cached_slots(
+    int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
+    int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
+    const dpf_block* seeds_in, const uint8_t* control_in, int64_t in_stride,
+    const int32_t* parent, const dpf_block* path, const int32_t* save_index, dpf_block* seeds_out,
+    uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed, const uint8_t* cw_left,
+    const uint8_t* cw_right, const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+    const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
+    const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
+    dpf_block* leaf_cache, int64_t leaf_stride, const int32_t* leaf_slot, void* stream) {
   int st = validate_desc(desc);
   if (st) return st;
   const int max_e = dpf_hip_prefix_batch_max_expand(desc, sum);
@@ -786,11 +810,17 @@ int dpf_hip_eval_prefix_batch_cached(
     if (leaf_cache) {
       if (leaf_stride < (num_starts << expand_levels))
         return fail(kInvalidArgument, "expansion cache too small");
-      if (seeds_in && (const void*)leaf_cache < (const void*)(seeds_in + num_keys * in_stride) &&
+      // In place (leaf_cache == seeds_in) only through a slot table, whose
+      // contract (include/dpf_hip.h) keeps every entry's read before its write.
+      const bool in_place =
+          leaf_slot && leaf_cache == seeds_in && in_stride == leaf_stride && !control_in;
+      if (seeds_in && !in_place &&
+          (const void*)leaf_cache < (const void*)(seeds_in + num_keys * in_stride) &&
           (const void*)seeds_in < (const void*)(leaf_cache + num_keys * leaf_stride))
         return fail(kInvalidArgument, "expansion cache overlaps the start seeds");
       p.leaf_seeds = leaf_cache;
       p.leaf_stride = leaf_stride;
+      p.leaf_slot = leaf_slot;
     }
     p.rkl = expand_key(key_left);
     p.rkr = expand_key(key_right);
@@ -828,6 +858,7 @@ int dpf_hip_eval_prefix_batch_cached(
       a.wide = p.wide;
       a.leaf_seeds = p.leaf_seeds;
       a.leaf_stride = p.leaf_stride;
+      a.leaf_slot = p.leaf_slot;
       a.nl = nl;
       a.b = b;
       for (int k = 0; k < nl; ++k) a.mod[k] = (uint32_t)desc->mod_low[k];

@@ -78,6 +78,7 @@ struct HHParams {
   unsigned long long* wide;  // [start << 2 | leaf][nl][3]
   dpf_block* leaf_seeds;     // NULL: no expansion cache written
   int64_t leaf_stride;
+  const int32_t* leaf_slot;  // NULL: leaf i of start node u at slot (u << 2) + i
   Div32 div[2];
   RoundKeys rkl, rkr, rkv;
 };
@@ -104,7 +105,7 @@ __device__ __forceinline__ uint32_t mod_add(uint32_t a, uint32_t b, uint32_t n) 
 }
 
 // MMO hashes of two leaves' blocks x0, x0 + 1, x1, x1 + 1 (cc:500-524), ILP4.
-__device__ __forceinline__ void hash_leaf_pair(const LdsLookup& lk, const uint32_t* rkv, Block4 x0,
+__device__ __forceinline__ void hash_leaf_pair(const LdsLookup& lk, KeyRef rkv, Block4 x0,
                                                Block4 x1, Block4 h[4]) {
   const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
 #if DPF_HH_RESIGMA
@@ -136,7 +137,8 @@ void hh_level_kernel(HHParams p) {
   uint32_t m1;
   asm volatile("v_mov_b32 %0, 0xff00" : "=v"(m1));
   const LdsLookup lk{reinterpret_cast<const char*>(lds.tab),
-                     {lt, lt + 128u, lt + 65536u, lt + 65664u}, m1};
+                     {lt, lt + 128u, lt + 65536u, lt + 65664u}, m1,
+                     KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), KeyRef{}}};
   const int64_t U = p.num_starts;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.num_threads;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -173,7 +175,7 @@ void hh_level_kernel(HHParams p) {
       const uint32_t cc0 = (uint32_t)(p.cw_left[cwi] & 1) | ((uint32_t)(p.cw_right[cwi] & 1) << 1);
       Block4 c0, c1;
       uint32_t t0, t1;
-      children_step(lk, p.rkl.k, p.rkr.k, s, t, cs0, cc0, c0, t0, c1, t1);
+      children_step(lk, lk.ks.l, lk.ks.r, s, t, cs0, cc0, c0, t0, c1, t1);
       const uint4 cs1 = make_uint4(
           (uint32_t)p.cw_seed[cwi + 1].low, (uint32_t)(p.cw_seed[cwi + 1].low >> 32),
           (uint32_t)p.cw_seed[cwi + 1].high, (uint32_t)(p.cw_seed[cwi + 1].high >> 32));
@@ -181,22 +183,28 @@ void hh_level_kernel(HHParams p) {
           (uint32_t)(p.cw_left[cwi + 1] & 1) | ((uint32_t)(p.cw_right[cwi + 1] & 1) << 1);
       Block4 L[4];
       uint32_t tl[4];
-      children_step_x2(lk, p.rkl.k, p.rkr.k, c0, t0, c1, t1, cs1, cc1, L, tl);
+      children_step_x2(lk, lk.ks.l, lk.ks.r, c0, t0, c1, t1, cs1, cc1, L, tl);
       if (p.leaf_seeds && valid) {
-        dpf_block* o = p.leaf_seeds + k * p.leaf_stride + (u << 2);
+        // A slot table places the leaves when the cache is rewritten in place:
+        // leaf 0 in this node's own slot (read above by this thread), the
+        // others in slots no start node reads.
+        dpf_block* o = p.leaf_seeds + k * p.leaf_stride;
+        int4 sl = make_int4((int)(u << 2), (int)(u << 2) + 1, (int)(u << 2) + 2, (int)(u << 2) + 3);
+        if (p.leaf_slot) sl = *reinterpret_cast<const int4*>(p.leaf_slot + (u << 2));
+        const int slot[4] = {sl.x, sl.y, sl.z, sl.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           Block4 c = L[i];
           c.w0 |= tl[i];
-          store_block(o + i, c);
+          store_block(o + slot[i], c);
         }
       }
       // Value hashes (cc:500-524): two leaves' b blocks per ILP4 group.
       const int party = p.party[k] & 1;
       const dpf_block* vc = p.vcw + k * p.vcw_stride;
       const uint32_t corr[2] = {(uint32_t)vc[0].low, p.nl > 1 ? (uint32_t)vc[1].low : 0u};
-      const UniformRK rk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
-                               UniformRK{p.rkv.k}};
+      const UniformRK rk[4] = {UniformRK{lk.ks.v}, UniformRK{lk.ks.v}, UniformRK{lk.ks.v},
+                               UniformRK{lk.ks.v}};
 #if DPF_HH_STASH
       lds.stash[0][threadIdx.x] = make_uint4(L[2].w0 | tl[2], L[2].w1, L[2].w2, L[2].w3);
       lds.stash[1][threadIdx.x] = make_uint4(L[3].w0 | tl[3], L[3].w1, L[3].w2, L[3].w3);
@@ -215,7 +223,7 @@ void hh_level_kernel(HHParams p) {
 #endif
         Block4 h[4];
         if (p.b == 2) {
-          hash_leaf_pair(lk, p.rkv.k, L[2 * pr], L[2 * pr + 1], h);
+          hash_leaf_pair(lk, lk.ks.v, L[2 * pr], L[2 * pr + 1], h);
         } else {
           h[0] = L[2 * pr];
           h[2] = L[2 * pr + 1];
@@ -294,6 +302,7 @@ int launch_hh_level(const HHLevelArgs& a, hipStream_t s) {
   p.wide = a.wide;
   p.leaf_seeds = a.leaf_seeds;
   p.leaf_stride = a.leaf_stride;
+  p.leaf_slot = a.leaf_slot;
   for (int i = 0; i < a.nl; ++i) p.div[i] = make_div32(a.mod[i]);
   p.rkl = expand_key(a.key_left);
   p.rkr = expand_key(a.key_right);

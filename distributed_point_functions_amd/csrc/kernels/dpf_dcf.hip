@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int n = lv.n;
   const int dmax = lv.depth[n - 1];
   for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
@@ -81,9 +81,9 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
       Block4 hv = s, hn = s;
       if (FAST) {
         if (d < dmax)
-          dpf_aes::mmo_hash2(hv, hn, lk, UniformRK{p.rkv.k}, SelectRK{p.rkl.k, p.rkd.k, 0u - bit});
+          dpf_aes::mmo_hash2(hv, hn, lk, UniformRK{lk.ks.v}, SelectRK{lk.ks.l, lk.ks.d, 0u - bit});
         else
-          hv = dpf_aes::mmo_hash(s, lk, UniformRK{p.rkv.k});
+          hv = dpf_aes::mmo_hash(s, lk, UniformRK{lk.ks.v});
       }
       for (; level < n && lv.depth[level] == d; ++level) {
         const bool take = ((shr128(x, n - 1 - level)) & 1) == 0;  // current_bit == 0
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
           lf.vcw = vcw;
           lf.party = party;
           char buf[16 * kDcfMaxLeaves];
-          lf.convert_store(lk, p.rkv.k, s, t, bi, 1, buf);
+          lf.convert_store(lk, lk.ks.v, s, t, bi, 1, buf);
           int off = 0;
           for (int e = 0; e < nl; ++e) {
             const int lb = g.d.bits[e] >> 3;
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
         s = hn;
         t = nt;
       } else {
-        path_step(lk, p.rkl, p.rkd, s, t, bit, cs, cctl);
+        path_step(lk, lk.ks.l, lk.ks.d, s, t, bit, cs, cctl);
       }
     }
     char* o = p.out + u * (int64_t)p.esz;
@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_fast_kernel(DcfFast
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int n = p.n;
   using Acc = typename std::conditional<BITS == 128, u128, uint64_t>::type;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (g >> 6) < p.num_groups;
@@ -247,8 +247,8 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_fast_kernel(DcfFast
         for (int j = 0; j < ITEMS; ++j) {
           h[j] = s[j];
           h[ITEMS + j] = s[j];
-          rv[j] = UniformRK{p.rkv.k};
-          rs[j] = SelectRK{p.rkl.k, p.rkd.k, 0u - pb[j]};
+          rv[j] = UniformRK{lk.ks.v};
+          rs[j] = SelectRK{lk.ks.l, lk.ks.d, 0u - pb[j]};
         }
         dpf_aes::mmo_hashAB<ITEMS, ITEMS>(h, lk, rv, rs);
       } else {
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_fast_kernel(DcfFast
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
           h[j] = s[j];
-          rv[j] = UniformRK{p.rkv.k};
+          rv[j] = UniformRK{lk.ks.v};
         }
         dpf_aes::mmo_hashN<ITEMS>(h, lk, rv);
       }

@@ -102,6 +102,41 @@ __device__ __forceinline__ void fill_cws(LdsImage& lds, const dpf_block* cw_seed
   }
 }
 
+// Round keys of one AES key held as ONE VGPR: lane i keeps word i (i < 44),
+// read as a wave-uniform value with v_readlane (an SGPR; no memory access).
+// The kernel-argument form (DPF_RK_LANES=0) reloads a round's words with
+// s_load inside the rolled round loops, and SMEM returns out of order behind
+// the same lgkmcnt as the table lookups, so every first use of a reloaded
+// word waited lgkmcnt(0) for all lookups in flight.
+// key_ref must run where all lanes 0..43 of the wave are active (kernel
+// entry; workgroups are whole waves).
+#ifndef DPF_RK_LANES
+#define DPF_RK_LANES 0
+#endif
+#if DPF_RK_LANES
+struct KeyRef {
+  uint32_t v;
+};
+__device__ __forceinline__ KeyRef key_ref(const RoundKeys& rk) {
+  const int l = threadIdx.x & 63;
+  return KeyRef{rk.k[l < 44 ? l : 43]};
+}
+__device__ __forceinline__ uint32_t rk_word(KeyRef k, int i) {
+  return __builtin_amdgcn_readlane(k.v, i);
+}
+#else
+struct KeyRef {
+  const uint32_t* k;
+};
+__device__ __forceinline__ KeyRef key_ref(const RoundKeys& rk) { return KeyRef{rk.k}; }
+__device__ __forceinline__ uint32_t rk_word(KeyRef k, int i) { return k.k[i]; }
+#endif
+
+// The four keys of a launch (left, right, value, left ^ right) as KeyRefs.
+struct KeySet {
+  KeyRef l, r, v, d;
+};
+
 // Conflict-free LDS T-table lookup with ONE VALU of addressing: v_perm_b32
 // builds the byte address {lane offset, byte K of w, table half, 0}, i.e.
 // (entry << 8) | lt[T] with lt[T] = (lane & 31) * 4 (+128 for T1/T3, +64 KiB
@@ -115,6 +150,7 @@ struct LdsLookup {
   const char* base;
   uint32_t lt[4];
   uint32_t m1;  // 0xff00 in a VGPR
+  KeySet ks;    // the launch's round keys (set by make_lookup(lds, keys))
   template <int T, int K>
   __device__ __forceinline__ uint32_t lookup(uint32_t w) const {
     uint32_t off;
@@ -132,6 +168,14 @@ struct LdsLookup {
   __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) const {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
   }
+  // The same lookup through the vector memory pipe (aes_core.h DPF_L1_ROUNDS):
+  // T0 from a 1 KiB constant table (L1-resident after the first touches),
+  // T1..T3 as its byte rotations.
+  template <int T, int K>
+  __device__ __forceinline__ uint32_t l1(uint32_t w) const {
+    const uint32_t v = c_t0.v[(w >> (8 * K)) & 0xffu];
+    return T == 0 ? v : __builtin_amdgcn_alignbit(v, v, 32 - 8 * T);
+  }
 };
 
 __device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds) {
@@ -139,16 +183,21 @@ __device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds) {
   uint32_t m1;
   asm volatile("v_mov_b32 %0, 0xff00" : "=v"(m1));
   return LdsLookup{reinterpret_cast<const char*>(lds.tab), {l, l + 128u, l + 65536u, l + 65664u},
-                   m1};
+                   m1, KeySet{}};
+}
+__device__ __forceinline__ LdsLookup make_lookup(const LdsImage& lds, KeySet ks) {
+  LdsLookup lk = make_lookup(lds);
+  lk.ks = ks;
+  return lk;
 }
 
-// Round keys shared by the whole wave (kernel-argument resident).
+// Round keys shared by the whole wave.
 struct UniformRK {
-  const uint32_t* k;
-  __device__ __forceinline__ uint32_t operator()(int i) const { return k[i]; }
+  KeyRef k;
+  __device__ __forceinline__ uint32_t operator()(int i) const { return rk_word(k, i); }
   template <class LK>
   __device__ __forceinline__ uint32_t mix(const LK& lk, uint32_t a, uint32_t b, int i) const {
-    return lk.xor3(a, b, k[i]);
+    return lk.xor3(a, b, rk_word(k, i));
   }
 };
 // Per-lane key choice: rk = left ^ (mask & (left ^ right)).  In a round's last
@@ -156,14 +205,17 @@ struct UniformRK {
 // instruction reading one scalar key word (a VALU op reads at most one SGPR;
 // the plain form needed a v_mov of the key word first).
 struct SelectRK {
-  const uint32_t* left;
-  const uint32_t* diff;
+  KeyRef left;
+  KeyRef diff;
   uint32_t mask;
-  __device__ __forceinline__ uint32_t operator()(int i) const { return left[i] ^ (mask & diff[i]); }
+  __device__ __forceinline__ uint32_t operator()(int i) const {
+    return rk_word(left, i) ^ (mask & rk_word(diff, i));
+  }
   template <class LK>
   __device__ __forceinline__ uint32_t mix(const LK& lk, uint32_t a, uint32_t b, int i) const {
     // bitop3 truth table index = S0*4 + S1*2 + S2; 0x78 = S0 ^ (S1 & S2).
-    return __builtin_amdgcn_bitop3_b32(lk.xor3(a, b, left[i]), mask, diff[i], 0x78);
+    return __builtin_amdgcn_bitop3_b32(lk.xor3(a, b, rk_word(left, i)), mask, rk_word(diff, i),
+                                       0x78);
   }
 };
 
@@ -207,7 +259,7 @@ __device__ __forceinline__ Block4 add_small(Block4 s, uint32_t j) {
 
 // One tree step for a uniformly chosen child: seed/control correction and
 // control-bit extraction in the order of distributed_point_function.cc:323-343.
-__device__ __forceinline__ void child_step(const LdsLookup& lk, const uint32_t* rk, Block4 s,
+__device__ __forceinline__ void child_step(const LdsLookup& lk, KeyRef rk, Block4 s,
                                            uint32_t t, uint32_t dir, uint4 cs, uint32_t cctl,
                                            Block4& out, uint32_t& tout) {
   Block4 h = dpf_aes::mmo_hash(s, lk, UniformRK{rk});
@@ -221,8 +273,8 @@ __device__ __forceinline__ void child_step(const LdsLookup& lk, const uint32_t* 
 }
 
 // Both children of one node: two interleaved MMO hashes (left key, right key).
-__device__ __forceinline__ void children_step(const LdsLookup& lk, const uint32_t* rkl,
-                                              const uint32_t* rkr, Block4 s, uint32_t t, uint4 cs,
+__device__ __forceinline__ void children_step(const LdsLookup& lk, KeyRef rkl,
+                                              KeyRef rkr, Block4 s, uint32_t t, uint4 cs,
                                               uint32_t cctl, Block4& c0, uint32_t& t0, Block4& c1,
                                               uint32_t& t1) {
   Block4 h0 = s, h1 = s;
@@ -240,8 +292,8 @@ __device__ __forceinline__ void children_step(const LdsLookup& lk, const uint32_
 
 // children_step for two nodes of the same level (same correction word): the
 // four child hashes interleaved (ILP4).
-__device__ __forceinline__ void children_step_x2(const LdsLookup& lk, const uint32_t* rkl,
-                                                 const uint32_t* rkr, Block4 sa, uint32_t ta,
+__device__ __forceinline__ void children_step_x2(const LdsLookup& lk, KeyRef rkl,
+                                                 KeyRef rkr, Block4 sa, uint32_t ta,
                                                  Block4 sb, uint32_t tb, uint4 cs, uint32_t cctl,
                                                  Block4* c, uint32_t* t) {
   Block4 h[4] = {sa, sa, sb, sb};
@@ -259,10 +311,10 @@ __device__ __forceinline__ void children_step_x2(const LdsLookup& lk, const uint
 }
 
 // Path step with a per-lane direction bit (evaluate_prg_hwy.cc:452-486).
-__device__ __forceinline__ void path_step(const LdsLookup& lk, const RoundKeys& rkl,
-                                          const RoundKeys& rkd, Block4& s, uint32_t& t,
+__device__ __forceinline__ void path_step(const LdsLookup& lk, KeyRef rkl,
+                                          KeyRef rkd, Block4& s, uint32_t& t,
                                           uint32_t bit, uint4 cs, uint32_t cctl) {
-  Block4 h = dpf_aes::mmo_hash(s, lk, SelectRK{rkl.k, rkd.k, 0u - bit});
+  Block4 h = dpf_aes::mmo_hash(s, lk, SelectRK{rkl, rkd, 0u - bit});
   uint32_t m = 0u - t;
   h.w0 ^= cs.x & m; h.w1 ^= cs.y & m; h.w2 ^= cs.z & m; h.w3 ^= cs.w & m;
   uint32_t nt = h.w0 & 1u;
@@ -381,12 +433,12 @@ struct FastIntLeaf {
   }
 
   // Full-domain leaf: write elements_per_leaf elements.
-  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+  __device__ __forceinline__ void emit(const LdsLookup& lk, KeyRef rkv, Block4 seed,
                                        uint32_t t, int64_t leaf, char* out) const {
     store(correct(dpf_aes::mmo_hash(seed, lk, UniformRK{rkv}), t), leaf, out);
   }
   // Two sibling leaves (leaf, leaf + 1), hashed as one interleaved pair.
-  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+  __device__ __forceinline__ void emit2(const LdsLookup& lk, KeyRef rkv, Block4 s0,
                                         uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
                                         char* out) const {
     dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{rkv}, UniformRK{rkv});
@@ -402,7 +454,7 @@ struct FastIntLeaf {
     }
   }
   // Four consecutive leaves, hashed as one interleaved quadruple.
-  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, KeyRef rkv, Block4* s,
                                         const uint32_t* t, int64_t leaf, char* out) const {
     const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
     dpf_aes::mmo_hashN<4>(s, lk, rk);
@@ -542,12 +594,12 @@ struct SwarLeaf {
     if (party == 1) x = neg(x);
     return Block4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)(x >> 64), (uint32_t)(x >> 96)};
   }
-  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+  __device__ __forceinline__ void emit(const LdsLookup& lk, KeyRef rkv, Block4 seed,
                                        uint32_t t, int64_t leaf, char* out) const {
     store_packed(out + leaf * (int64_t)store_bytes,
                  correct(dpf_aes::mmo_hash(seed, lk, UniformRK{rkv}), t), store_bytes);
   }
-  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+  __device__ __forceinline__ void emit2(const LdsLookup& lk, KeyRef rkv, Block4 s0,
                                         uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
                                         char* out) const {
     dpf_aes::mmo_hash2(s0, s1, lk, UniformRK{rkv}, UniformRK{rkv});
@@ -557,7 +609,7 @@ struct SwarLeaf {
   // The half-octet's four value hashes as one ILP4 group, then the stores
   // (Tuple<u32, u64>: 18.65 -> 18.12 ms per 2^30 outputs vs two ILP2 pairs,
   // profiles/r11_ws_ab.txt).
-  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, KeyRef rkv, Block4* s,
                                         const uint32_t* t, int64_t leaf, char* out) const {
 #if DPF_SWAR_ILP4
     const UniformRK rk[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
@@ -623,7 +675,7 @@ struct Mod32Leaf {
       }
     }
   }
-  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+  __device__ __forceinline__ void emit(const LdsLookup& lk, KeyRef rkv, Block4 seed,
                                        uint32_t t, int64_t leaf, char* out) const {
     uint32_t w[8];
     Block4 h0 = seed, h1 = add_small(seed, 1u);
@@ -639,7 +691,7 @@ struct Mod32Leaf {
   }
   // The value blocks (seed, seed + 1) of two leaves as words w0[8], w1[8]
   // (b == 2: one interleaved quadruple of hashes).
-  __device__ __forceinline__ void hash2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+  __device__ __forceinline__ void hash2(const LdsLookup& lk, KeyRef rkv, Block4 s0,
                                         Block4 s1, uint32_t (&w0)[8], uint32_t (&w1)[8]) const {
     Block4 h[4] = {s0, add_small(s0, 1u), s1, add_small(s1, 1u)};
     if (b == 2) {
@@ -654,7 +706,7 @@ struct Mod32Leaf {
     w1[0] = h[2].w0; w1[1] = h[2].w1; w1[2] = h[2].w2; w1[3] = h[2].w3;
     w1[4] = h[3].w0; w1[5] = h[3].w1; w1[6] = h[3].w2; w1[7] = h[3].w3;
   }
-  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+  __device__ __forceinline__ void emit2(const LdsLookup& lk, KeyRef rkv, Block4 s0,
                                         uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
                                         char* out) const {
     uint32_t w0[8], w1[8];
@@ -665,7 +717,7 @@ struct Mod32Leaf {
   // Four consecutive leaves (leaf % 4 == 0), converted first and stored as
   // whole 16-byte pieces: 32 contiguous bytes per lane for pairs (nl == 2),
   // 16 for single elements -- not four 8-byte stores spread over the AES work.
-  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, KeyRef rkv, Block4* s,
                                         const uint32_t* t, int64_t leaf, char* out) const {
     uint32_t x[4][NLMAX];
 #pragma unroll
@@ -734,7 +786,7 @@ struct GenericLeaf {
 
   // Hashes `seed` into b blocks and writes element `first .. first+count` of the
   // converted array (after correction) to out_elem.
-  __device__ void convert_store(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+  __device__ void convert_store(const LdsLookup& lk, KeyRef rkv, Block4 seed,
                                 uint32_t t, int first, int count, char* out_elem) const {
     uint8_t bytes[16 * kBMax];
     const int b = d.blocks_needed;
@@ -798,18 +850,18 @@ struct GenericLeaf {
     }
   }
 
-  __device__ __forceinline__ void emit(const LdsLookup& lk, const uint32_t* rkv, Block4 seed,
+  __device__ __forceinline__ void emit(const LdsLookup& lk, KeyRef rkv, Block4 seed,
                                        uint32_t t, int64_t leaf, char* out) const {
     convert_store(lk, rkv, seed, t, 0, elements_per_leaf,
                   out + leaf * (int64_t)elements_per_leaf * esz);
   }
-  __device__ __forceinline__ void emit2(const LdsLookup& lk, const uint32_t* rkv, Block4 s0,
+  __device__ __forceinline__ void emit2(const LdsLookup& lk, KeyRef rkv, Block4 s0,
                                         uint32_t t0, Block4 s1, uint32_t t1, int64_t leaf,
                                         char* out) const {
     emit(lk, rkv, s0, t0, leaf, out);
     emit(lk, rkv, s1, t1, leaf + 1, out);
   }
-  __device__ __forceinline__ void emit4(const LdsLookup& lk, const uint32_t* rkv, Block4* s,
+  __device__ __forceinline__ void emit4(const LdsLookup& lk, KeyRef rkv, Block4* s,
                                         const uint32_t* t, int64_t leaf, char* out) const {
     for (int i = 0; i < 4; ++i) emit(lk, rkv, s[i], t[i], leaf + i, out);
   }
@@ -822,12 +874,12 @@ __device__ __forceinline__ uint32_t path_bit(Block4 p, int pos) {
 }
 
 // Two path steps with per-lane directions, interleaved (evaluate_prg_hwy.cc:452-486).
-__device__ __forceinline__ void path_step2(const LdsLookup& lk, const RoundKeys& rkl,
-                                           const RoundKeys& rkd, Block4& s0, uint32_t& t0,
+__device__ __forceinline__ void path_step2(const LdsLookup& lk, KeyRef rkl,
+                                           KeyRef rkd, Block4& s0, uint32_t& t0,
                                            uint32_t b0, Block4& s1, uint32_t& t1, uint32_t b1,
                                            uint4 cs, uint32_t cctl) {
   Block4 h0 = s0, h1 = s1;
-  dpf_aes::mmo_hash2(h0, h1, lk, SelectRK{rkl.k, rkd.k, 0u - b0}, SelectRK{rkl.k, rkd.k, 0u - b1});
+  dpf_aes::mmo_hash2(h0, h1, lk, SelectRK{rkl, rkd, 0u - b0}, SelectRK{rkl, rkd, 0u - b1});
   uint32_t m0 = 0u - t0, m1 = 0u - t1;
   h0.w0 ^= cs.x & m0; h0.w1 ^= cs.y & m0; h0.w2 ^= cs.z & m0; h0.w3 ^= cs.w & m0;
   h1.w0 ^= cs.x & m1; h1.w1 ^= cs.y & m1; h1.w2 ^= cs.z & m1; h1.w3 ^= cs.w & m1;
@@ -895,7 +947,7 @@ __device__ __forceinline__ void wide_xor(unsigned long long* w, u128 v) {
 
 // Packed-element conversion for the generic path: element `e` of the hashed
 // leaf, corrected and negated, as per-leaf values.
-__device__ void generic_point_values(const GenericLeaf& g, const LdsLookup& lk, const uint32_t* rkv,
+__device__ void generic_point_values(const GenericLeaf& g, const LdsLookup& lk, KeyRef rkv,
                                      Block4 seed, uint32_t t, int e, const dpf_block* vcw,
                                      int party, u128* vals) {
   char buf[16 * DPF_MAX_LEAVES];

@@ -24,6 +24,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <atomic>
 #include <chrono>
@@ -68,10 +69,11 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void hash_kernel(int64_t n, 
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
-  LdsLookup lk = make_lookup(lds);
+  const KeyRef kr = key_ref(rk);
+  LdsLookup lk = make_lookup(lds, KeySet{kr, kr, kr, kr});
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    store_block(out + i, dpf_aes::mmo_hash(load_block(in + i), lk, UniformRK{rk.k}));
+    store_block(out + i, dpf_aes::mmo_hash(load_block(in + i), lk, UniformRK{lk.ks.v}));
   }
 }
 
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_paths_kernel(PathP
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
   __syncthreads();
-  LdsLookup lk = make_lookup(lds);
+  LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, KeyRef{}, key_ref(p.rkd)});
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p.n;
        i += (int64_t)gridDim.x * blockDim.x) {
     Block4 s = load_block(p.seeds_in + i);
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_paths_kernel(PathP
     Block4 path = load_block(p.paths + i);
     for (int j = 0; j < p.num_levels; ++j) {
       uint32_t bit = path_bit(path, p.num_levels - 1 - j);
-      path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
+      path_step(lk, lk.ks.l, lk.ks.d, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
     }
     store_block(p.seeds_out + i, s);
     p.ctrl_out[i] = (uint8_t)t;
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
   const int k0 = p.k0, S = p.S;
   const int B = S >= 1 ? 1 : 0;  // leaf pairs share their parent
   const int G = S - B;            // depth of the DFS stack
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
     uint32_t t = p.ctrl_in[r] & 1u;
     for (int j = 0; j < k0; ++j) {
       uint32_t bit = (uint32_t)((item >> (k0 - 1 - j)) & 1);
-      path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
+      path_step(lk, lk.ks.l, lk.ks.d, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
     }
     // 2. depth-first over the subtree.  Every inner node is expanded into both
     //    children at once (two interleaved hashes); the left child is descended
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
       for (int d = ds; d < G; ++d) {
         Block4 c0, c1;
         uint32_t t0, t1;
-        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d],
+        children_step(lk, lk.ks.l, lk.ks.r, node, nt, lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d],
                       c0, t0, c1, t1);
 #pragma unroll
         for (int e = 1; e <= kGMax; ++e)
@@ -162,14 +164,14 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
         nt = t0;
       }
       if (B == 0) {
-        leaf.emit(lk, p.rkv.k, node, nt, leaf_base + g, p.out);
+        leaf.emit(lk, lk.ks.v, node, nt, leaf_base + g, p.out);
       } else {
         const int lvl = k0 + G;
         Block4 c0, c1;
         uint32_t t0, t1;
-        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c0, t0,
+        children_step(lk, lk.ks.l, lk.ks.r, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c0, t0,
                       c1, t1);
-        leaf.emit2(lk, p.rkv.k, c0, t0, c1, t1, leaf_base + 2 * g, p.out);
+        leaf.emit2(lk, lk.ks.v, c0, t0, c1, t1, leaf_base + 2 * g, p.out);
       }
     }
   }
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
 // whole blocks store 4 x 16 contiguous bytes; other policies use their emit4.
 template <int BITS, bool XOR>
 __device__ __forceinline__ void octet_half(const FastIntLeaf<BITS, XOR>& leaf, const LdsLookup& lk,
-                                           const uint32_t* rkv, Block4* l, const uint32_t* lt,
+                                           KeyRef rkv, Block4* l, const uint32_t* lt,
                                            int64_t first_leaf, char* out) {
   const UniformRK rv[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
   dpf_aes::mmo_hashN<4>(l, lk, rv);
@@ -206,7 +208,7 @@ __device__ __forceinline__ void octet_half(const FastIntLeaf<BITS, XOR>& leaf, c
 }
 template <class Leaf>
 __device__ __forceinline__ void octet_half(const Leaf& leaf, const LdsLookup& lk,
-                                           const uint32_t* rkv, Block4* l, const uint32_t* lt,
+                                           KeyRef rkv, Block4* l, const uint32_t* lt,
                                            int64_t first_leaf, char* out) {
   leaf.emit4(lk, rkv, l, lt, first_leaf, out);
 }
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
   const int k0 = p.k0, S = p.S;
   const int G = S - 3;
   const int64_t ngroups = (int64_t)1 << G;
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
     uint32_t t = p.ctrl_in[r] & 1u;
     for (int j = 0; j < k0; ++j) {
       const uint32_t bit = (uint32_t)((item >> (k0 - 1 - j)) & 1);
-      path_step(lk, p.rkl, p.rkd, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
+      path_step(lk, lk.ks.l, lk.ks.d, s, t, bit, lds.cw_seed[j], lds.cw_ctrl[j]);
     }
     // 2. depth-first down to the octet roots; right children parked in
     //    sib[d] (scratch), their control bits in tb.
@@ -269,7 +271,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
       for (int d = ds; d < G; ++d) {
         Block4 c0, c1;
         uint32_t t0, t1;
-        children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d],
+        children_step(lk, lk.ks.l, lk.ks.r, node, nt, lds.cw_seed[k0 + d], lds.cw_ctrl[k0 + d],
                       c0, t0, c1, t1);
         sib[d] = c1;
         tb = (tb & ~(1u << (d + 1))) | (t1 << (d + 1));
@@ -282,9 +284,9 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
       const int lvl = k0 + G;
       Block4 c[2], q[4];
       uint32_t ct[2], qt[4];
-      children_step(lk, p.rkl.k, p.rkr.k, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c[0],
+      children_step(lk, lk.ks.l, lk.ks.r, node, nt, lds.cw_seed[lvl], lds.cw_ctrl[lvl], c[0],
                     ct[0], c[1], ct[1]);
-      children_step_x2(lk, p.rkl.k, p.rkr.k, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
+      children_step_x2(lk, lk.ks.l, lk.ks.r, c[0], ct[0], c[1], ct[1], lds.cw_seed[lvl + 1],
                        lds.cw_ctrl[lvl + 1], q, qt);
       // The second half's two grandchildren wait outside the VGPRs during the
       // first half (OctetStash: lane-private LDS slots, else scratch beside
@@ -322,11 +324,11 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
             q[3] = sib[kGMax - 1];
           }
         }
-        children_step_x2(lk, p.rkl.k, p.rkr.k, q[2 * hf], qt[2 * hf], q[2 * hf + 1],
+        children_step_x2(lk, lk.ks.l, lk.ks.r, q[2 * hf], qt[2 * hf], q[2 * hf + 1],
                          qt[2 * hf + 1], lds.cw_seed[lvl + 2], lds.cw_ctrl[lvl + 2], l, lt);
         // The half's four value hashes (ILP4), conversion, correction, stores
         // (integer leaves: 64 contiguous bytes per lane).
-        octet_half(leaf, lk, p.rkv.k, l, lt, leaf_base + 8 * g + 4 * hf, p.out);
+        octet_half(leaf, lk, lk.ks.v, l, lt, leaf_base + 8 * g + 4 * hf, p.out);
       }
     }
   }
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(Poin
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int L = p.num_levels;
   const int64_t P = p.points_per_key, half = p.half;
   for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
@@ -428,17 +430,17 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(Poin
         const uint4 cs = make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
                                     (uint32_t)(c.high >> 32));
         if constexpr (PAIRED)
-          path_step2(lk, p.rkl, p.rkd, s0, t0, b0, s1, t1, b1, cs, cctl);
+          path_step2(lk, lk.ks.l, lk.ks.d, s0, t0, b0, s1, t1, b1, cs, cctl);
         else
-          path_step(lk, p.rkl, p.rkd, s0, t0, b0, cs, cctl);
+          path_step(lk, lk.ks.l, lk.ks.d, s0, t0, b0, cs, cctl);
       }
       const dpf_block* vcw = p.vcw + k * p.vcw_stride;
       if constexpr (FAST) {
         Block4 h0 = s0, h1 = s1;
         if constexpr (PAIRED)
-          dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{p.rkv.k}, UniformRK{p.rkv.k});
+          dpf_aes::mmo_hash2(h0, h1, lk, UniformRK{lk.ks.v}, UniformRK{lk.ks.v});
         else
-          h0 = dpf_aes::mmo_hash(h0, lk, UniformRK{p.rkv.k});
+          h0 = dpf_aes::mmo_hash(h0, lk, UniformRK{lk.ks.v});
         const u128 v0 = fast_point_value<BITS>(h0, t0, bi0, dpf_u128(vcw[bi0]), party, p.xor_mode);
         const u128 v1 =
             PAIRED ? fast_point_value<BITS>(h1, t1, bi1, dpf_u128(vcw[bi1]), party, p.xor_mode) : v0;
@@ -452,17 +454,17 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(Poin
       } else {
         if (SUM) {
           u128 v[DPF_MAX_LEAVES];
-          generic_point_values(leaf, lk, p.rkv.k, s0, t0, bi0, vcw, party, v);
+          generic_point_values(leaf, lk, lk.ks.v, s0, t0, bi0, vcw, party, v);
           for (int e = 0; e < nl; ++e) acc0[e] = leaf_group_add(leaf.d, e, acc0[e], v[e]);
-          generic_point_values(leaf, lk, p.rkv.k, s1, t1, bi1, vcw, party, v);
+          generic_point_values(leaf, lk, lk.ks.v, s1, t1, bi1, vcw, party, v);
           for (int e = 0; e < nl; ++e) acc1[e] = leaf_group_add(leaf.d, e, acc1[e], v[e]);
         } else {
           GenericLeaf lf = leaf;
           lf.vcw = vcw;
           lf.party = party;
-          lf.convert_store(lk, p.rkv.k, s0, t0, bi0, 1, p.out + (k * P + q0) * (int64_t)p.esz);
+          lf.convert_store(lk, lk.ks.v, s0, t0, bi0, 1, p.out + (k * P + q0) * (int64_t)p.esz);
           if (has1)
-            lf.convert_store(lk, p.rkv.k, s1, t1, bi1, 1, p.out + (k * P + q1) * (int64_t)p.esz);
+            lf.convert_store(lk, lk.ks.v, s1, t1, bi1, 1, p.out + (k * P + q1) * (int64_t)p.esz);
         }
       }
     }
@@ -664,7 +666,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(Poi
   __shared__ LdsImage lds;
   fill_tables(lds.tab);
   __syncthreads();
-  const LdsLookup lk = make_lookup(lds);
+  const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int L = p.num_levels;
   const int64_t P = p.points_per_key, quarter = p.half;
   // Sums of <= 64-bit values wrap mod 2^64 exactly (the group is mod 2^BITS).
@@ -715,7 +717,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(Poi
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           b[i] = path_bit(path[i], L - 1 - j + p.bib);
-          rk[i] = SelectRK{p.rkl.k, p.rkd.k, 0u - b[i]};
+          rk[i] = SelectRK{lk.ks.l, lk.ks.d, 0u - b[i]};
         }
         Block4 h[4] = {st[0], st[1], st[2], st[3]};
         dpf_aes::mmo_hashN<4>(h, lk, rk);
@@ -731,8 +733,8 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(Poi
         }
       }
       const dpf_block* vcw = p.vcw + k * p.vcw_stride;
-      const UniformRK vk[4] = {UniformRK{p.rkv.k}, UniformRK{p.rkv.k}, UniformRK{p.rkv.k},
-                               UniformRK{p.rkv.k}};
+      const UniformRK vk[4] = {UniformRK{lk.ks.v}, UniformRK{lk.ks.v}, UniformRK{lk.ks.v},
+                               UniformRK{lk.ks.v}};
       dpf_aes::mmo_hashN<4>(st, lk, vk);
       const uint32_t bmask = (1u << p.bib) - 1u;
 #pragma unroll
@@ -986,6 +988,28 @@ int bounce_d2h(void* dst, const void* src, size_t bytes, void* stream) {
 // profiles/r14_fresh_output_microbench.jsonl): 32 MiB 4.5 vs 3.9 ms, 256 MiB
 // 26.3 vs 25.9 ms; at 8 GiB the DMA straight into the range wins (42 vs ~28 GB/s).
 constexpr size_t kRegisterMin = DPF_HIP_REGISTER_MIN_BYTES;
+// The 512 MiB threshold prices the page faults of FRESH destinations.  A host
+// range whose pages are already mapped -- every H2D source, and D2H
+// destinations the caller has touched -- costs ~2 us/MiB to register (16 ms
+// for 8 GiB, tools/host_output_microbench.cc) against a DMA at ~57 GB/s
+// instead of ~12 GB/s through the bounce buffers, so those register from
+// 32 MiB (the r13 threshold); profiles/r15_mapped_register_ab.txt.
+// DPF_HIP_REGISTER_MAPPED_MIB=<n> (read per call) overrides it: the A/B hook.
+size_t register_min_mapped() {
+  const char* v = std::getenv("DPF_HIP_REGISTER_MAPPED_MIB");
+  const long m = v && *v ? std::strtol(v, nullptr, 10) : 0;
+  return m > 0 ? static_cast<size_t>(m) << 20 : size_t{32} << 20;
+}
+// First, middle and last page of [p, p + bytes) resident (mincore): the
+// range was touched before, so registering it maps no fresh pages.
+bool pages_mapped(const void* p, size_t bytes) {
+  const uintptr_t pg = 4096, lo = reinterpret_cast<uintptr_t>(p);
+  for (uintptr_t a : {lo, lo + bytes / 2, lo + bytes - 1}) {
+    unsigned char v = 0;
+    if (mincore(reinterpret_cast<void*>(a & ~(pg - 1)), pg, &v) != 0 || !(v & 1)) return false;
+  }
+  return true;
+}
 constexpr size_t kStagedChunk = size_t{64} << 20;
 
 // The library's own transient registrations, reference-counted: a second
@@ -1009,7 +1033,8 @@ enum Acquire { kNotOurs, kAcquired, kOverlaps };
 // kOverlaps: part of the range is in a registration of ours -- the copy must
 // take the bounce path (HIP would take the partly registered range as
 // page-locked).  kNotOurs: use the page-locked test / bounce path.
-Acquire acquire_host(void* p, size_t bytes, bool reuse_only, uintptr_t* base) {
+Acquire acquire_host(void* p, size_t bytes, bool reuse_only, uintptr_t* base,
+                     size_t min_bytes = kRegisterMin) {
   const uintptr_t lo = reinterpret_cast<uintptr_t>(p), hi = lo + bytes;
   std::lock_guard<std::mutex> lock(g_reg_mu);
   auto it = g_regs.upper_bound(lo);
@@ -1025,7 +1050,7 @@ Acquire acquire_host(void* p, size_t bytes, bool reuse_only, uintptr_t* base) {
     }
   }
   if (it != g_regs.end() && it->first < hi) return kOverlaps;  // overlaps the one above
-  if (reuse_only || bytes < kRegisterMin) return kNotOurs;
+  if (reuse_only || bytes < min_bytes) return kNotOurs;
   if (hipHostRegister(p, bytes, hipHostRegisterDefault) != hipSuccess) {
     (void)hipGetLastError();
     return kNotOurs;
@@ -1034,6 +1059,16 @@ Acquire acquire_host(void* p, size_t bytes, bool reuse_only, uintptr_t* base) {
   g_reg_count.store(static_cast<int>(g_regs.size()));
   *base = lo;
   return kAcquired;
+}
+
+// True if [lo, hi) overlaps a registration of ours (g_reg_mu held).
+bool overlaps_registration(uintptr_t lo, uintptr_t hi) {
+  auto it = g_regs.upper_bound(lo);
+  if (it != g_regs.begin()) {
+    auto prev = std::prev(it);
+    if (prev->first + prev->second.bytes > lo) return true;
+  }
+  return it != g_regs.end() && it->first < hi;
 }
 
 void release_host(uintptr_t base) {
@@ -1186,13 +1221,20 @@ int pipelined_d2h(char* h, const char* d, size_t bytes, void (*before)(void*, si
       int st = -1;
       if (limit >= 0 && static_cast<long>(i) >= limit) {
         // test hook: refused
-      } else if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
-        std::lock_guard<std::mutex> lock(g_reg_mu);
-        g_regs[cut[i]] = Registration{len, 1};
-        g_reg_count.store(static_cast<int>(g_regs.size()));
-        st = 1;
       } else {
-        (void)hipGetLastError();
+        // Under g_reg_mu from the overlap check to the insert: another thread
+        // may have registered part of this piece since acquire_host said
+        // kNotOurs.  An overlapping piece is refused (the bounce path).
+        std::lock_guard<std::mutex> lock(g_reg_mu);
+        if (!overlaps_registration(cut[i], cut[i + 1])) {
+          if (hipHostRegister(p, len, hipHostRegisterDefault) == hipSuccess) {
+            g_regs[cut[i]] = Registration{len, 1};
+            g_reg_count.store(static_cast<int>(g_regs.size()));
+            st = 1;
+          } else {
+            (void)hipGetLastError();
+          }
+        }
       }
       t_fault += std::chrono::duration<double>(b - a).count();
       t_reg += std::chrono::duration<double>(clk::now() - b).count();
@@ -1327,8 +1369,9 @@ int dpf_hip_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
   uintptr_t base = 0;
   if (bytes >= kBounceMin || g_reg_count.load() > 0) {
     // Inside a registration of ours (another thread's copy), or large and new.
-    const Acquire a =
-        acquire_host(const_cast<void*>(src), bytes, bytes < kBounceMin || page_locked(src), &base);
+    const Acquire a = acquire_host(const_cast<void*>(src), bytes,
+                                   bytes < kBounceMin || page_locked(src), &base,
+                                   register_min_mapped());
     if (a == kAcquired)
       return registered_copy((char*)const_cast<void*>(src), (char*)dst, bytes, false, nullptr,
                              nullptr, (hipStream_t)stream, base);
@@ -1359,7 +1402,10 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
   if (!bytes) return kOk;
   uintptr_t base = 0;
   if (bytes >= kBounceMin || g_reg_count.load() > 0) {
-    const Acquire a = acquire_host(dst, bytes, bytes < kBounceMin || page_locked(dst), &base);
+    const bool reuse_only = bytes < kBounceMin || page_locked(dst);
+    const Acquire a =
+        acquire_host(dst, bytes, reuse_only, &base,
+                     !reuse_only && pages_mapped(dst, bytes) ? register_min_mapped() : kRegisterMin);
     if (a == kAcquired)
       return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true, nullptr,
                              nullptr, (hipStream_t)stream, base);
@@ -1441,7 +1487,14 @@ int dpf_hip_memcpy_d2h_chunked(const void* src, size_t bytes, size_t align,
     if (i + 1 < n)
       HIP_TRY(hipMemcpyAsync(g_bounce[(i + 1) & 1], (const char*)src + (i + 1) * chunk, len(i + 1),
                              hipMemcpyDeviceToHost, s));
-    consume(ctx, g_bounce[i & 1], i * chunk, len(i));
+    // The next chunk's DMA into the other bounce buffer must have finished
+    // before the buffers (and g_bounce_mu) are given up on any path out.
+    try {
+      consume(ctx, g_bounce[i & 1], i * chunk, len(i));
+    } catch (...) {
+      (void)hipStreamSynchronize(s);
+      return fail(kInternal, "dpf_hip_memcpy_d2h_chunked: consume threw");
+    }
   }
   return kOk;
 }

@@ -49,6 +49,7 @@ struct HHLevelArgs {
   unsigned long long* wide;
   dpf_block* leaf_seeds;
   int64_t leaf_stride;
+  const int32_t* leaf_slot;  // NULL: leaf i of start node u at slot (u << 2) + i
   int nl, b;
   uint32_t mod[2];
   const dpf_aes_key* key_left;

@@ -104,7 +104,11 @@ class Server:
         self.out = torch.empty(max_outputs * 8, dtype=torch.uint8, device=device)
 
     def reset(self) -> None:
+        """Restarts at the first level; keeps the expansion cache's buffers."""
         self.ctx.reset()
+
+    def release_expansion_cache(self) -> None:
+        self.ctx.release_expansion_cache()
 
     def evaluate(self, level: int, prefixes: Sequence[int], stream=None) -> int:
         return self.dpf.evaluate_until_batch_to_device(level, prefixes, self.ctx, self.out,
@@ -130,11 +134,14 @@ def select(values: Sequence[int], counts: np.ndarray, top_k: int) -> List[int]:
 
 def run(dpf, servers: Sequence[Server], logs: Sequence[int], top_k: int = 1024,
         aggregate: Optional[Callable] = None, stream=None,
-        record: Optional[list] = None) -> List[int]:
+        record: Optional[list] = None, keep_cache: bool = False) -> List[int]:
     """One full heavy-hitters pass over every hierarchy level.  `aggregate(level,
     packed_tensor, n)` combines per-rank sums (default: single rank).
     Returns the final candidates; appends (level, values, counts, tags) to
-    `record` when given."""
+    `record` when given.  The servers' expansion caches (up to 64 GiB per
+    buffer at 2^20 clients) are given back after the last level unless
+    `keep_cache` -- a caller running pass after pass keeps them (regrowing
+    them costs seconds per pass) and releases them itself afterwards."""
     prefixes: List[int] = []
     for h, log in enumerate(logs):
         step = log - (logs[h - 1] if h else 0)
@@ -155,6 +162,11 @@ def run(dpf, servers: Sequence[Server], logs: Sequence[int], top_k: int = 1024,
         if record is not None:
             record.append((h, values, counts.copy(), tot[:, 1].copy()))
         prefixes = select(values, counts, top_k)
+    if not keep_cache:
+        for srv in servers:
+            release = getattr(srv, "release_expansion_cache", None)
+            if release is not None:
+                release()
     return prefixes  # the heavy hitters of the last level
 
 

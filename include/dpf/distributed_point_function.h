@@ -180,21 +180,13 @@ class DistributedPointFunction {
   template <typename T>
   StatusOr<std::vector<T>> EvaluateAt(const DpfKey& key, int hierarchy_level,
                                       Span<const uint128> evaluation_points) const {
-    ValueType t = ToValueType<T>();
-    StatusOr<std::vector<uint8_t>> packed =
-        EvaluateAtPacked(key, hierarchy_level, evaluation_points, nullptr, &t);
-    if (!packed.ok()) return packed.status();
-    return Unpack<T>(hierarchy_level, *packed);
+    return EvaluateAtImpl<T>(key, hierarchy_level, evaluation_points, nullptr);
   }
 
   template <typename T>
   StatusOr<std::vector<T>> EvaluateAt(int hierarchy_level, Span<const uint128> evaluation_points,
                                       EvaluationContext& ctx) const {
-    ValueType t = ToValueType<T>();
-    StatusOr<std::vector<uint8_t>> packed =
-        EvaluateAtPacked(ctx.key(), hierarchy_level, evaluation_points, &ctx, &t);
-    if (!packed.ok()) return packed.status();
-    return Unpack<T>(hierarchy_level, *packed);
+    return EvaluateAtImpl<T>(ctx.key(), hierarchy_level, evaluation_points, &ctx);
   }
 
   Span<const DpfParameters> parameters() const { return validator_->parameters(); }
@@ -230,6 +222,11 @@ class DistributedPointFunction {
                                                   Span<const uint128> evaluation_points,
                                                   EvaluationContext* ctx,
                                                   const ValueType* requested_type = nullptr) const;
+  // EvaluateAt's packed output copied into `sink` (EvaluateAt<T>: straight
+  // into the returned std::vector<T>).
+  Status EvaluateAtToHost(const DpfKey& key, int hierarchy_level,
+                          Span<const uint128> evaluation_points, EvaluationContext* ctx,
+                          const ValueType* requested_type, const HostSink& sink) const;
   // keys[k] is evaluated at points[k*points_per_key .. (k+1)*points_per_key).
   StatusOr<std::vector<uint8_t>> EvaluateAtBatchPacked(Span<const DpfKey* const> keys,
                                                        int hierarchy_level,
@@ -323,6 +320,26 @@ class DistributedPointFunction {
                            std::vector<int> blocks_needed, std::vector<dpf_internal::FlatValueType> flat,
                            Aes128FixedKeyHash prg_left, Aes128FixedKeyHash prg_right,
                            Aes128FixedKeyHash prg_value);
+
+  // EvaluateAt<T> (h:839-1010): the packed output copied or unpacked into
+  // the result chunk by chunk, as EvaluateUntil<T> does.
+  template <typename T>
+  StatusOr<std::vector<T>> EvaluateAtImpl(const DpfKey& key, int hierarchy_level,
+                                          Span<const uint128> evaluation_points,
+                                          EvaluationContext* ctx) const {
+    ValueType t = ToValueType<T>();
+    std::vector<T> out;
+    if constexpr (dpf_internal::kPackedIsMemoryImage<T>) {
+      const HostSink sink = dpf_internal::VectorSink(&out);
+      Status status = EvaluateAtToHost(key, hierarchy_level, evaluation_points, ctx, &t, sink);
+      if (!status.ok()) return status;
+    } else {
+      const HostSink sink = dpf_internal::UnpackSink(&flat_, hierarchy_level, &out);
+      Status status = EvaluateAtToHost(key, hierarchy_level, evaluation_points, ctx, &t, sink);
+      if (!status.ok()) return status;
+    }
+    return out;
+  }
 
   template <typename T>
   StatusOr<std::vector<T>> Unpack(int h, const std::vector<uint8_t>& packed) const {

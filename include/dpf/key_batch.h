@@ -121,6 +121,7 @@ class DeviceBatchContext {
     int64_t cache_refused = 0;   // no room for the cache: the call wrote none
     int64_t spare_refused = 0;   // no room for a spare: start seeds gathered, cache rewritten in place
     int64_t in_place = 0;        // calls that gathered their start seeds, then rewrote the cache
+    int64_t permuted = 0;        // calls that rewrote the cache in place through a slot table (no gather)
     int64_t evicted_spare = 0;   // spare freed so a per-call buffer fits
     int64_t evicted_cache = 0;   // unread cache freed so a per-call buffer fits
     int64_t alloc_failures = 0;  // per-call allocations that failed (before any eviction)
@@ -163,8 +164,14 @@ class DeviceBatchContext {
   // from the partial evaluations two calls back).  leaf_de_: levels from a
   // tree index of that call to its leaves.  Double-buffered: a call reads
   // leaf_seeds_ and writes leaf_spare_, then the two swap; without room for
-  // the spare, the start seeds are gathered (slots_) and the cache is
-  // rewritten in place.
+  // the spare the kernel rewrites the cache in place, each leaf into a slot
+  // that only its own thread reads or nobody reads (leaf_phys_: logical leaf
+  // -> physical slot, empty = identity), and when no such slot table exists
+  // the start seeds are gathered first (slots_).  leaf_stride_ is the
+  // physical row stride.
+  std::vector<int32_t> leaf_phys_;
+  void* leaf_slot_ = nullptr;  // device copy of the slot table of the running call
+  size_t leaf_slot_cap_ = 0;
   void* leaf_seeds_ = nullptr;  // seed | control bit (bit 0)
   size_t leaf_seeds_cap_ = 0;
   void* leaf_spare_ = nullptr;

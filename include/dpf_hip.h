@@ -101,8 +101,11 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
  * piece by piece on a helper thread while the DMA fills the pieces already
  * registered), others go through page-locked staging.  The drop-in
  * EvaluateUntil<T> returns its std::vector<T> this way. */
-/* Host ranges of at least this many bytes are registered (page-locked) for a
- * copy and DMAed straight into; smaller ones go through page-locked staging. */
+/* FRESH host ranges (pages not yet mapped) of at least this many bytes are
+ * registered (page-locked) for a copy and DMAed straight into; smaller ones go
+ * through page-locked staging.  Ranges whose pages are already mapped (every
+ * dpf_hip_memcpy_h2d source; dpf_hip_memcpy_d2h destinations the caller has
+ * touched) are registered from 32 MiB. */
 #define DPF_HIP_REGISTER_MIN_BYTES ((size_t)512 << 20)
 
 /* D2H copy handed to the host chunk by chunk: the bytes arrive in the
@@ -341,6 +344,30 @@ int dpf_hip_eval_prefix_batch_cached(
     const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
     const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
     dpf_block* leaf_cache, int64_t leaf_stride, void* stream);
+
+/* dpf_hip_eval_prefix_batch_cached with the cache rewritten IN PLACE:
+ * leaf l of start node u goes to leaf_cache[k*leaf_stride + leaf_slot[(u <<
+ * expand_levels) + l]] (leaf_slot: device, num_starts << expand_levels
+ * entries), and leaf_cache may be seeds_in itself (in_stride == leaf_stride,
+ * control_in == NULL).  Contract on the table: a slot that
+ * some start node reads (parent[u]) may appear only among the leaves of that
+ * start node, and only if no other start node reads it; every other entry is
+ * a slot no start node reads.  Each (key, start node) is one thread that
+ * reads its start seed before it writes any leaf, so no entry is overwritten
+ * before it has been read -- no gather of the start seeds and no second
+ * cache buffer (the heavy-hitters steady state at 2^20
+ * clients, where a 64 GiB spare does not fit).  leaf_slot == NULL: exactly
+ * dpf_hip_eval_prefix_batch_cached. */
+int dpf_hip_eval_prefix_batch_cached_slots(
+    int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
+    int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
+    const dpf_block* seeds_in, const uint8_t* control_in, int64_t in_stride,
+    const int32_t* parent, const dpf_block* path, const int32_t* save_index, dpf_block* seeds_out,
+    uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed, const uint8_t* cw_left,
+    const uint8_t* cw_right, const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+    const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
+    const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
+    dpf_block* leaf_cache, int64_t leaf_stride, const int32_t* leaf_slot, void* stream);
 
 /* seeds_out[k*num_rows + i] / control_out[k*num_rows + i] = the seed (bit 0
  * cleared) and control bit (bit 0) of cache[k*cache_stride + slot[i]]: a

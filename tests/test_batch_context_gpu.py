@@ -165,6 +165,36 @@ def test_batch_incremental_cache_in_place(levels, plan, sum_mode, monkeypatch):
     _run(levels, plan, 37, sum_mode, seed=len(levels) + 13)
 
 
+@pytest.mark.parametrize("levels,plan", CASES[:4] + CASES[-3:], ids=lambda x: str(x)[:60])
+@pytest.mark.parametrize("sum_mode", [False, True])
+def test_batch_incremental_cache_permuted(levels, plan, sum_mode, monkeypatch):
+    """DPF_BATCH_CACHE_MODE=permute: no spare; the kernel rewrites the cache
+    in place through a slot table (each start node's leaf 0 into the slot it
+    read, the other leaves into slots no start node reads; several start
+    nodes per tree index leave their shared slot alone).  Same outputs and
+    contexts, and no gather once the cache stride has stopped growing."""
+    monkeypatch.setenv("DPF_BATCH_CACHE_MODE", "permute")
+    _, bctx = _run(levels, plan, 37, sum_mode, seed=len(levels) + 17)
+    ev = bctx.cache_events
+    assert ev["evicted_spare"] == 0 and ev["evicted_cache"] == 0, ev
+    if levels is HH5[0]:
+        assert ev["permuted"] >= 1, ev
+
+
+def test_permuted_cache_hh_shape_reads_and_writes_one_buffer(monkeypatch):
+    """Heavy-hitters shape (Tuple<IntModN32 x2>, 2-bit steps, all candidates
+    kept): every cached level after the stride stops growing is a permuted
+    in-place rewrite, and the context never holds a second cache buffer."""
+    levels, plan = HH5
+    bctx0, _, held0 = _pressure_run(levels, plan, 40, True, seed=97)
+    assert bctx0.cache_events["permuted"] == 0      # default: a spare fits
+    monkeypatch.setenv("DPF_BATCH_CACHE_MODE", "permute")
+    bctx, failed, held = _pressure_run(levels, plan, 40, True, seed=97)
+    ev = bctx.cache_events
+    assert failed == [] and ev["permuted"] >= 1 and ev["spare_refused"] == 0, ev
+    assert max(held) < max(held0)          # the spare run holds two cache buffers
+
+
 def test_batch_many_prefixes_one_key():
     """Config-5a shape: one key, thousands of prefixes per level."""
     import torch

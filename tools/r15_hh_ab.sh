@@ -1,0 +1,10 @@
+#!/bin/bash
+# r15 lease B: heavy hitters' expansion-cache modes, same box.  2^18 clients
+# (a spare fits): spare (default) / permuted in place / gather + in place;
+# 2^20 clients (no spare fits): permuted in place (default) / gather.
+set -u
+O=gpurun_out; mkdir -p $O
+bash tools/ab.sh --tag r15b_hh18 --rounds 2 -- "--workload heavy_hitters --keys-log 18" \
+  cur env:DPF_BATCH_CACHE_MODE=permute env:DPF_BATCH_CACHE_MODE=gather || exit 1
+bash tools/ab.sh --tag r15b_hh20 --rounds 1 -- "--workload heavy_hitters" \
+  cur env:DPF_BATCH_CACHE_MODE=gather || exit 1
