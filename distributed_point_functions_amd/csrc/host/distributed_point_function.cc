@@ -830,19 +830,20 @@ namespace {
 // checks = the fused domain check + path / block-index pass over the points,
 // key = key validation, value correction, context lookups and correction
 // words, upload = the one packed H2D, launch = the point kernel's launch,
-// copy = waiting for the kernel + the D2H into the caller's vector (unpacked
-// chunk by chunk).
+// device = waiting for the upload and the kernel (timing runs only: the
+// stream is synchronised there), copy = the D2H into the caller's vector
+// (unpacked chunk by chunk).
 struct AtTiming {
-  double t[5] = {0, 0, 0, 0, 0};
+  double t[6] = {0, 0, 0, 0, 0, 0};
   long calls = 0;
   ~AtTiming() {
     const double n = static_cast<double>(calls - 10);
     if (calls > 10 && std::getenv("DPF_HOST_TIMING"))
       std::fprintf(stderr,
                    "[EvaluateAt host timing] calls=%ld per call: checks=%.2fus key=%.2fus "
-                   "upload=%.2fus launch=%.2fus copy=%.2fus\n",
+                   "upload=%.2fus launch=%.2fus device=%.2fus copy=%.2fus\n",
                    calls, t[0] * 1e6 / n, t[1] * 1e6 / n, t[2] * 1e6 / n, t[3] * 1e6 / n,
-                   t[4] * 1e6 / n);
+                   t[4] * 1e6 / n, t[5] * 1e6 / n);
   }
 };
 AtTiming g_at_timing;
@@ -980,12 +981,16 @@ Status DistributedPointFunction::EvaluateAtToHost(const DpfKey& key, int hierarc
       nullptr));
   DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
   clk.mark(3);
+  if (g_until_timing_on) {
+    HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(nullptr));
+    clk.mark(4);
+  }
   // Packed elements straight into the caller's result (h:983-1003 outputs):
   // integers copied, tuples / IntModN / XorWrapper unpacked chunk by chunk out
   // of the page-locked staging buffers.
   HIP_RETURN_IF_ERROR(dpf_internal::CopyToHostSink(sink, sink.reserve(bytes), s->out.get(), bytes,
                                                    nullptr));
-  clk.mark(4);
+  clk.mark(5);
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();
 }
@@ -1011,61 +1016,91 @@ StatusOr<std::vector<uint8_t>> DistributedPointFunction::EvaluateAtBatchPacked(
   const uint128 max_point =
       log_domain_size < 128 ? (static_cast<uint128>(1) << log_domain_size) - 1 : Uint128Max();
   const int64_t n = static_cast<int64_t>(points.size());
-  for (int64_t i = 0; i < n; ++i)
-    if (points[i] > max_point)
-      return InvalidArgumentError("`evaluation_points[" + std::to_string(i) +
-                                  "]` larger than the domain size at hierarchy level " +
-                                  std::to_string(hierarchy_level));
-  if (n == 0) return std::vector<uint8_t>{};
   const dpf_internal::FlatValueType& f = flat_[hierarchy_level];
   const int E = f.elements_per_block, nl = static_cast<int>(f.leaves.size());
   const int L = hierarchy_to_tree()[hierarchy_level];
   const int bib = log_domain_size - L;
-  std::vector<dpf_block> seeds(num_keys), cw_seed(std::max<int64_t>(num_keys * L, 1));
-  std::vector<uint8_t> party(num_keys), cl(std::max<int64_t>(num_keys * L, 1)),
-      cr(std::max<int64_t>(num_keys * L, 1));
-  std::vector<dpf_block> vcw(num_keys * E * nl);
-  for (int64_t k = 0; k < num_keys; ++k) {
-    const DpfKey& key = *keys[k];
-    DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
-    seeds[k] = ToBlock(FromProtoBlock(key.seed()));
-    party[k] = static_cast<uint8_t>(key.party() & 1);
-    for (int j = 0; j < L; ++j) {
-      const CorrectionWord& cw = key.correction_words(j);
-      cw_seed[k * L + j] = ToBlock(FromProtoBlock(cw.seed()));
-      cl[k * L + j] = cw.control_left();
-      cr[k * L + j] = cw.control_right();
-    }
-    DPF_ASSIGN_OR_RETURN(std::vector<uint128> v, ValueCorrectionLeaves(key, hierarchy_level));
-    for (int i = 0; i < E * nl; ++i) vcw[k * E * nl + i] = ToBlock(v[i]);
-  }
-  std::vector<dpf_block> paths(n);
-  std::vector<int32_t> block_index(n, 0);
-  for (int64_t i = 0; i < n; ++i) {
-    paths[i] = ToBlock(E > 1 ? points[i] >> bib : points[i]);
-    if (E > 1) block_index[i] = static_cast<int32_t>(points[i] & ((static_cast<uint128>(1) << bib) - 1));
-  }
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
-  DPF_RETURN_IF_ERROR(s->Upload(s->key_seed, seeds.data(), seeds.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->party, party.data(), party.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->cw_seed, cw_seed.data(), cw_seed.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->cw_left, cl.data(), cl.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->cw_right, cr.data(), cr.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw.data(), vcw.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->paths, paths.data(), paths.size()));
-  DPF_RETURN_IF_ERROR(s->Upload(s->block_index, block_index.data(), block_index.size()));
-  DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(n) * f.packed_size));
+  PackedUploads& up = s->packed;
+  DPF_RETURN_IF_ERROR(up.Reset());
+  const int64_t rows = std::max<int64_t>(num_keys * L, 1);
+  up.Prepare(9 * 256 + static_cast<size_t>(n) * (sizeof(dpf_block) + sizeof(int32_t)) +
+             static_cast<size_t>(num_keys) * (sizeof(dpf_block) + 1 + E * nl * sizeof(dpf_block)) +
+             static_cast<size_t>(rows) * (sizeof(dpf_block) + 2) + 64);
+  // The points: domain check, tree indices and block indices in one threaded
+  // pass into the upload image (EvaluateAt's order: points before keys).
+  size_t o_paths, o_bi;
+  dpf_block* paths = up.Reserve<dpf_block>(n, &o_paths);
+  int32_t* block_index = up.Reserve<int32_t>(n, &o_bi);
+  const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
+  const int64_t bad = CheckAndFillPoints(points, max_point, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      paths[i] = ToBlock(E > 1 ? points[i] >> bib : points[i]);
+      block_index[i] = E > 1 ? static_cast<int32_t>(points[i] & bmask) : 0;
+    }
+  });
+  if (bad < n)
+    return InvalidArgumentError("`evaluation_points[" + std::to_string(bad) +
+                                "]` larger than the domain size at hierarchy level " +
+                                std::to_string(hierarchy_level));
+  if (n == 0) return std::vector<uint8_t>{};
+  // The keys: validated and flattened (SoA, [key][level]) on host threads;
+  // the first failing key's error is returned.
+  size_t o_seed, o_party, o_cws, o_cl, o_cr, o_vcw;
+  dpf_block* seeds = up.Reserve<dpf_block>(num_keys, &o_seed);
+  uint8_t* party = up.Reserve<uint8_t>(num_keys, &o_party);
+  dpf_block* cw_seed = up.Reserve<dpf_block>(rows, &o_cws);
+  uint8_t* cl = up.Reserve<uint8_t>(rows, &o_cl);
+  uint8_t* cr = up.Reserve<uint8_t>(rows, &o_cr);
+  dpf_block* vcw = up.Reserve<dpf_block>(std::max<int64_t>(num_keys * E * nl, 1), &o_vcw);
+  std::atomic<int64_t> first_bad{num_keys};
+  dpf_internal::ParallelFor(
+      num_keys,
+      [&](int64_t lo, int64_t hi) {
+        for (int64_t k = lo; k < hi; ++k) {
+          const DpfKey& key = *keys[k];
+          StatusOr<std::vector<uint128>> v = validator_->ValidateDpfKey(key).ok()
+                                                 ? ValueCorrectionLeaves(key, hierarchy_level)
+                                                 : StatusOr<std::vector<uint128>>(
+                                                       InvalidArgumentError("invalid key"));
+          if (!v.ok()) {
+            int64_t cur = first_bad.load();
+            while (k < cur && !first_bad.compare_exchange_weak(cur, k)) {
+            }
+            return;
+          }
+          seeds[k] = ToBlock(FromProtoBlock(key.seed()));
+          party[k] = static_cast<uint8_t>(key.party() & 1);
+          for (int j = 0; j < L; ++j) {
+            const CorrectionWord& cw = key.correction_words(j);
+            cw_seed[k * L + j] = ToBlock(FromProtoBlock(cw.seed()));
+            cl[k * L + j] = cw.control_left();
+            cr[k * L + j] = cw.control_right();
+          }
+          for (int i = 0; i < E * nl; ++i) vcw[k * E * nl + i] = ToBlock((*v)[i]);
+        }
+      },
+      int64_t{256});
+  if (first_bad.load() < num_keys) {
+    // The failing key's own error, as the one-by-one loop reported it.
+    const DpfKey& key = *keys[first_bad.load()];
+    DPF_RETURN_IF_ERROR(validator_->ValidateDpfKey(key));
+    return ValueCorrectionLeaves(key, hierarchy_level).status();
+  }
+  DPF_RETURN_IF_ERROR(up.Commit(nullptr));
+  const size_t bytes = static_cast<size_t>(n) * f.packed_size;
+  DPF_RETURN_IF_ERROR(s->out.Reserve(bytes));
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
   HIP_RETURN_IF_ERROR(dpf_hip_eval_points(
-      n, points_per_key, L, s->key_seed.as<dpf_block>(), s->party.as<uint8_t>(), nullptr, nullptr,
-      s->paths.as<dpf_block>(), s->block_index.as<int32_t>(), s->cw_seed.as<dpf_block>(),
-      s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr, &kv, &desc,
-      s->vcw.as<dpf_block>(), s->out.get(), nullptr));
+      n, points_per_key, L, up.Ptr<dpf_block>(o_seed), up.Ptr<uint8_t>(o_party), nullptr, nullptr,
+      up.Ptr<dpf_block>(o_paths), up.Ptr<int32_t>(o_bi), up.Ptr<dpf_block>(o_cws),
+      up.Ptr<uint8_t>(o_cl), up.Ptr<uint8_t>(o_cr), &kl, &kr, &kv, &desc,
+      up.Ptr<dpf_block>(o_vcw), s->out.get(), nullptr));
+  DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
   std::vector<uint8_t> out;
-  HIP_RETURN_IF_ERROR(CopyToHostVector(&out, s->out.get(),
-                                       static_cast<size_t>(n) * f.packed_size, nullptr));
+  HIP_RETURN_IF_ERROR(CopyToHostVector(&out, s->out.get(), bytes, nullptr));
   return out;
 }
 

@@ -119,7 +119,12 @@ struct KeyRef {
 };
 __device__ __forceinline__ KeyRef key_ref(const RoundKeys& rk) {
   const int l = threadIdx.x & 63;
-  return KeyRef{rk.k[l < 44 ? l : 43]};
+  uint32_t v = rk.k[l < 44 ? l : 43];
+  // Pins the load at kernel entry (every lane active): without it the
+  // compiler sank it into divergent code, where inactive lanes never loaded
+  // their word and v_readlane read garbage (wrong outputs, r15).
+  asm volatile("" : "+v"(v));
+  return KeyRef{v};
 }
 __device__ __forceinline__ uint32_t rk_word(KeyRef k, int i) {
   return __builtin_amdgcn_readlane(k.v, i);

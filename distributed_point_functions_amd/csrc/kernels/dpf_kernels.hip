@@ -993,7 +993,7 @@ constexpr size_t kRegisterMin = DPF_HIP_REGISTER_MIN_BYTES;
 // destinations the caller has touched -- costs ~2 us/MiB to register (16 ms
 // for 8 GiB, tools/host_output_microbench.cc) against a DMA at ~57 GB/s
 // instead of ~12 GB/s through the bounce buffers, so those register from
-// 32 MiB (the r13 threshold); profiles/r15_mapped_register_ab.txt.
+// 32 MiB (the r13 threshold); profiles/r15_ab.txt (3), r15_mapped_register_ab.jsonl.
 // DPF_HIP_REGISTER_MAPPED_MIB=<n> (read per call) overrides it: the A/B hook.
 size_t register_min_mapped() {
   const char* v = std::getenv("DPF_HIP_REGISTER_MAPPED_MIB");
