@@ -3,6 +3,15 @@
 // dpf/internal/value_type_helpers.{h,cc} and dpf/int_mod_n.{h,cc} unless noted).
 #include "dpf/internal/value_type_helpers.h"
 
+#include <pthread.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <exception>
+#include <mutex>
+#include <thread>
+
 #include <sys/mman.h>
 
 #include <cmath>
@@ -392,6 +401,146 @@ void PrefaultPages(void* p, size_t bytes) {
   ParallelChunks(pages, NumChunks(pages, 4096), [base](int, int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) base[i * kPage] = 0;
   });
+}
+
+namespace {
+// The persistent worker pool behind RunOnPool (host_util.h).  Workers and
+// the caller spin briefly on the job generation / completion counters before
+// sleeping, so back-to-back parallel loops (the ~10-100 us phases of one
+// EvaluateAt call) do not pay a futex wake-up per worker.
+class WorkerPool {
+ public:
+  explicit WorkerPool(int workers) {
+    for (int i = 0; i < workers; ++i) threads_.emplace_back([this] { Loop(); });
+  }
+  int workers() const { return static_cast<int>(threads_.size()); }
+  // False if another thread's job is running.
+  bool TryRun(int chunks, const std::function<void(int)>& fn) {
+    std::unique_lock<std::mutex> submit(submit_, std::try_to_lock);
+    if (!submit.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      fn_ = &fn;
+      chunks_ = chunks;
+      next_.store(0);
+      error_ = nullptr;
+      active_.store(workers());
+      gen_.fetch_add(1, std::memory_order_release);
+    }
+    cv_.notify_all();
+    Work(chunks, fn);
+    SpinUntil([this] { return active_.load(std::memory_order_acquire) == 0; });
+    if (active_.load(std::memory_order_acquire) != 0) {
+      std::unique_lock<std::mutex> lock(mu_);
+      done_cv_.wait(lock, [this] { return active_.load() == 0; });
+    }
+    std::lock_guard<std::mutex> lock(mu_);
+    fn_ = nullptr;
+    if (error_) std::rethrow_exception(error_);
+    return true;
+  }
+  static thread_local bool in_worker;
+
+ private:
+  // Polls `done` for up to ~50 us (yielding the CPU between polls: a pause
+  // loop can cost a VM exit per iteration on virtualised hosts), then gives up.
+  template <typename P>
+  static void SpinUntil(P done) {
+    const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(50);
+    while (!done()) {
+      for (int i = 0; i < 64 && !done(); ++i) {
+      }
+      if (done() || std::chrono::steady_clock::now() > until) return;
+      std::this_thread::yield();
+    }
+  }
+  void Work(int chunks, const std::function<void(int)>& fn) {
+    for (int c = next_.fetch_add(1); c < chunks; c = next_.fetch_add(1)) {
+      try {
+        fn(c);
+      } catch (...) {
+        std::lock_guard<std::mutex> lock(mu_);
+        if (!error_) error_ = std::current_exception();
+      }
+    }
+  }
+  void Loop() {
+    in_worker = true;
+    uint64_t seen = 0;
+    for (;;) {
+      SpinUntil([&] { return gen_.load(std::memory_order_acquire) != seen; });
+      const std::function<void(int)>* fn;
+      int chunks;
+      {
+        std::unique_lock<std::mutex> lock(mu_);
+        cv_.wait(lock, [&] { return gen_.load() != seen; });
+        seen = gen_.load();
+        fn = fn_;
+        chunks = chunks_;
+      }
+      Work(chunks, *fn);
+      if (active_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        std::lock_guard<std::mutex> lock(mu_);
+        done_cv_.notify_one();
+      }
+    }
+  }
+  std::mutex submit_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int chunks_ = 0;
+  std::atomic<int> next_{0};
+  std::atomic<int> active_{0};
+  std::atomic<uint64_t> gen_{0};
+  std::exception_ptr error_;
+  std::vector<std::thread> threads_;
+};
+thread_local bool WorkerPool::in_worker = false;
+
+// Never destroyed (its threads wait for work until the process exits); a
+// forked child starts a pool of its own (the parent's threads do not exist
+// there).
+std::atomic<WorkerPool*> g_pool{nullptr};
+std::mutex g_pool_mu;
+WorkerPool* Pool() {
+  WorkerPool* p = g_pool.load();
+  if (p) return p;
+  std::lock_guard<std::mutex> lock(g_pool_mu);
+  if (!g_pool.load()) {
+    static bool atfork = [] {
+      pthread_atfork(nullptr, nullptr, [] { g_pool.store(nullptr); });
+      return true;
+    }();
+    (void)atfork;
+    g_pool.store(new WorkerPool(std::max(HostThreads() - 1, 1)));
+  }
+  return g_pool.load();
+}
+}  // namespace
+
+void RunOnPool(int chunks, const std::function<void(int)>& fn) {
+  if (chunks <= 1 || WorkerPool::in_worker) {
+    for (int c = 0; c < chunks; ++c) fn(c);
+    return;
+  }
+  if (Pool()->TryRun(chunks, fn)) return;
+  // The pool is busy with another thread's job: threads of this call's own.
+  std::vector<std::thread> pool;
+  std::exception_ptr error;
+  std::mutex mu;
+  auto run = [&](int c) {
+    try {
+      fn(c);
+    } catch (...) {
+      std::lock_guard<std::mutex> lock(mu);
+      if (!error) error = std::current_exception();
+    }
+  };
+  pool.reserve(chunks - 1);
+  for (int c = 1; c < chunks; ++c) pool.emplace_back(run, c);
+  run(0);
+  for (auto& th : pool) th.join();
+  if (error) std::rethrow_exception(error);
 }
 
 void ParallelRanges(int64_t n, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
