@@ -732,6 +732,10 @@ struct Mod32Leaf {
       convert(w0, t[j], x[j]);
       convert(w1, t[j + 1], x[j + 1]);
     }
+    store4(x, leaf, out);
+  }
+  __device__ __forceinline__ void store4(const uint32_t (&x)[4][NLMAX], int64_t leaf,
+                                         char* out) const {
     if (NLMAX >= 2 && nl == 2) {
       constexpr int i1 = NLMAX >= 2 ? 1 : 0;
       uint4* o = reinterpret_cast<uint4*>(out + leaf * 8);

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandPar
 template <int BITS, bool XOR>
 __device__ __forceinline__ void octet_half(const FastIntLeaf<BITS, XOR>& leaf, const LdsLookup& lk,
                                            KeyRef rkv, Block4* l, const uint32_t* lt,
-                                           int64_t first_leaf, char* out) {
+                                           int64_t first_leaf, char* out, Block4*) {
   const UniformRK rv[4] = {UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}, UniformRK{rkv}};
   dpf_aes::mmo_hashN<4>(l, lk, rv);
   uint4* o = reinterpret_cast<uint4*>(out + first_leaf * 16);
@@ -209,8 +209,46 @@ __device__ __forceinline__ void octet_half(const FastIntLeaf<BITS, XOR>& leaf, c
 template <class Leaf>
 __device__ __forceinline__ void octet_half(const Leaf& leaf, const LdsLookup& lk,
                                            KeyRef rkv, Block4* l, const uint32_t* lt,
-                                           int64_t first_leaf, char* out) {
+                                           int64_t first_leaf, char* out, Block4* park) {
   leaf.emit4(lk, rkv, l, lt, first_leaf, out);
+}
+#ifndef DPF_MOD32_PARK
+#define DPF_MOD32_PARK 1
+#endif
+// Tuples of IntModN<uint32_t>: the half's second leaf pair (seed | control
+// bit in bit 0) waits in two scratch slots beside the DFS stack while the
+// first pair's four value hashes run, instead of in 8 + 2 VGPRs -- that group
+// was the register-starved one (~3 lookups in flight, r15 ISA).
+template <class Leaf> struct OctetStash;
+template <int NL>
+__device__ __forceinline__ void octet_half(const Mod32Leaf<NL>& leaf, const LdsLookup& lk,
+                                           KeyRef rkv, Block4* l, const uint32_t* lt,
+                                           int64_t first_leaf, char* out, Block4* park) {
+#if DPF_MOD32_PARK
+  static_assert(OctetStash<Mod32Leaf<NL>>::value >= 2, "park slots hold the octet stash");
+  park[0] = Block4{l[2].w0 | lt[2], l[2].w1, l[2].w2, l[2].w3};
+  park[1] = Block4{l[3].w0 | lt[3], l[3].w1, l[3].w2, l[3].w3};
+  asm volatile("" ::: "memory");   // read them back from scratch, not from registers
+  uint32_t x[4][NL];
+  {
+    uint32_t w0[8], w1[8];
+    leaf.hash2(lk, rkv, l[0], l[1], w0, w1);
+    leaf.convert(w0, lt[0], x[0]);
+    leaf.convert(w1, lt[1], x[1]);
+  }
+  asm volatile("" ::: "memory");
+  {
+    const Block4 a = park[0], b = park[1];
+    uint32_t w0[8], w1[8];
+    leaf.hash2(lk, rkv, Block4{a.w0 & ~1u, a.w1, a.w2, a.w3}, Block4{b.w0 & ~1u, b.w1, b.w2, b.w3},
+               w0, w1);
+    leaf.convert(w0, a.w0 & 1u, x[2]);
+    leaf.convert(w1, b.w0 & 1u, x[3]);
+  }
+  leaf.store4(x, first_leaf, out);
+#else
+  leaf.emit4(lk, rkv, l, lt, first_leaf, out);
+#endif
 }
 
 // Where the octet keeps its second half's two grandchildren during the first
@@ -328,7 +366,9 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
                          qt[2 * hf + 1], lds.cw_seed[lvl + 2], lds.cw_ctrl[lvl + 2], l, lt);
         // The half's four value hashes (ILP4), conversion, correction, stores
         // (integer leaves: 64 contiguous bytes per lane).
-        octet_half(leaf, lk, lk.ks.v, l, lt, leaf_base + 8 * g + 4 * hf, p.out);
+        // sib[kGMax - 2 ..] is free when the stash lives in LDS (kStash == 2):
+        // Mod32Leaf parks a leaf pair there.
+        octet_half(leaf, lk, lk.ks.v, l, lt, leaf_base + 8 * g + 4 * hf, p.out, &sib[kGMax - 2]);
       }
     }
   }
