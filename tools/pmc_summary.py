@@ -88,6 +88,17 @@ def main():
                    min_ns=min(sel), max_ns=max(sel))
         if a.total:
             res["passes"] = a.passes
+            # A pass of several kernels: `kernel` names them by share of the
+            # pass's device time (largest first), `kernels` has the split.
+            per_k = defaultdict(lambda: [0, 0])
+            for _, d, name, _ in durs:
+                per_k[name][0] += 1
+                per_k[name][1] += d
+            tot = sum(v[1] for v in per_k.values())
+            order = sorted(per_k.items(), key=lambda kv: -kv[1][1])
+            res["kernels"] = [{"kernel": k, "calls": v[0], "ns_per_pass": v[1] / a.passes,
+                               "share": v[1] / tot} for k, v in order]
+            res["kernel"] = " + ".join(k for k, _ in order)
     sums, launches = defaultdict(float), defaultdict(set)
     for f in glob.glob(os.path.join(a.dir, "p*", "*counter_collection.csv")):
         for row in csv.DictReader(open(f)):
