@@ -18,7 +18,7 @@
 # gpurun_out/<tag>_<workload>_summary.json (copied to profiles/ afterwards).
 # Usage (GPU box, repo root): bash tools/round_evidence.sh <tag> part1|part2|part3|part4
 set -u
-TAG=${1:-r14}; PART=${2:-part1}
+TAG=${1:-r15}; PART=${2:-part1}
 O=gpurun_out; mkdir -p $O
 export TMPDIR=/tmp
 prof() { bash tools/profile_workload.sh "$@" || exit 1; }
