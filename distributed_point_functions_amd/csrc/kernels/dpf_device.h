@@ -876,6 +876,95 @@ struct GenericLeaf {
   }
 };
 
+// ------------------------------------------------------------------------
+// Latency mode: one AES chain per lane QUAD.  A launch far below one wave per
+// SIMD (a small EvaluateAt call) is bound by how fast ONE chain walks its
+// path, and a lone wave issues a VALU op only every ~5 clk: the ~40
+// instructions of a one-lane round cost ~390 clk.  Here lane c of a quad
+// holds column c of the state and computes output column c of every round
+// (4 lookups, the other three columns fetched from its neighbours with DPP
+// quad permutes), so a round is ~12 instructions per lane.  Same arithmetic
+// as aes_core.h's encrypt: n_c = T0[b0(w_c)] ^ T1[b1(w_c+1)] ^ T2[b2(w_c+2)]
+// ^ T3[b3(w_c+3)] ^ rk_c.  Every lane of a quad must be active.
+// ------------------------------------------------------------------------
+namespace quad {
+// Lane c of a quad gets the value of lane (c + k) mod 4.
+template <int K>
+__device__ __forceinline__ uint32_t from_next(uint32_t v) {
+  constexpr int ctrl = K == 0 ? 0xE4
+                       : K == 1 ? (1 | 2 << 2 | 3 << 4 | 0 << 6)
+                       : K == 2 ? (2 | 3 << 2 | 0 << 4 | 1 << 6)
+                                : (3 | 0 << 2 | 1 << 4 | 2 << 6);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xf, 0xf, false);
+}
+// Lane 0's value in every lane of the quad.
+__device__ __forceinline__ uint32_t from_lane0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int column() { return (int)(threadIdx.x & 3); }
+
+// Column c's word of every round key, one VGPR per round (rounds unrolled).
+struct Keys {
+  uint32_t k[11];
+};
+__device__ __forceinline__ Keys keys_of(const RoundKeys& rk) {
+  Keys q;
+  const int c = column();
+#pragma unroll
+  for (int r = 0; r < 11; ++r) q.k[r] = rk.k[4 * r + c];
+  return q;
+}
+
+// sigma(x) = (x2, x3, x2 ^ x0, x3 ^ x1), column by column.
+__device__ __forceinline__ uint32_t sigma(uint32_t x) {
+  const uint32_t y = from_next<2>(x);
+  return column() < 2 ? y : (x ^ y);
+}
+
+// AES-128 of the quad's state (this lane: column c); round key word r of
+// this column = left.k[r] ^ (mask & diff.k[r]) (mask 0: left alone).
+__device__ __forceinline__ uint32_t encrypt(uint32_t w, const LdsLookup& lk, const Keys& left,
+                                            const Keys& diff, uint32_t mask) {
+  w ^= left.k[0] ^ (mask & diff.k[0]);
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t b = from_next<1>(w), c = from_next<2>(w), d = from_next<3>(w);
+    const uint32_t n = lk.xor3(lk.template lookup<0, 0>(w), lk.template lookup<1, 1>(b),
+                               lk.template lookup<2, 2>(c));
+    w = __builtin_amdgcn_bitop3_b32(lk.xor3(n, lk.template lookup<3, 3>(d), left.k[r]), mask,
+                                    diff.k[r], 0x78);
+  }
+  const uint32_t b = from_next<1>(w), c = from_next<2>(w), d = from_next<3>(w);
+  const uint32_t x = lk.template lookup<2, 0>(w), y = lk.template lookup<3, 1>(b);
+  const uint32_t z = lk.template lookup<0, 2>(c), u = lk.template lookup<1, 3>(d);
+  const uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
+  const uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
+  return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ left.k[10] ^ (mask & diff.k[10]);
+}
+__device__ __forceinline__ uint32_t mmo(uint32_t x, const LdsLookup& lk, const Keys& left,
+                                        const Keys& diff, uint32_t mask) {
+  const uint32_t s = sigma(x);
+  return encrypt(s, lk, left, diff, mask) ^ s;
+}
+// One path step (evaluate_prg_hwy.cc:452-486) of the quad's chain: bit,
+// t, cs (this column's word of the correction seed) and cctl are
+// quad-uniform.
+__device__ __forceinline__ void path_step(const LdsLookup& lk, const Keys& left, const Keys& diff,
+                                          uint32_t& s, uint32_t& t, uint32_t bit, uint32_t cs,
+                                          uint32_t cctl) {
+  uint32_t h = mmo(s, lk, left, diff, 0u - bit);
+  h ^= cs & (0u - t);
+  const uint32_t nt = (from_lane0(h) & 1u) ^ (t & ((cctl >> bit) & 1u));
+  if (column() == 0) h &= ~1u;
+  s = h;
+  t = nt;
+}
+// The quad's four columns in every lane, as a block (lane 0: in order).
+__device__ __forceinline__ Block4 gather(uint32_t w) {
+  return Block4{w, from_next<1>(w), from_next<2>(w), from_next<3>(w)};
+}
+}  // namespace quad
+
 // Path bit `pos` of a 128-bit path.
 __device__ __forceinline__ uint32_t path_bit(Block4 p, int pos) {
   uint32_t w = pos < 32 ? p.w0 : pos < 64 ? p.w1 : pos < 96 ? p.w2 : p.w3;

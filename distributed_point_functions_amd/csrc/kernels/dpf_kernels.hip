@@ -798,6 +798,62 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(Poi
   }
 }
 
+// Latency mode of eval_points_kernel<GenericLeaf, BITS, true, ..> for small
+// calls (no sum): one (key, point) per lane QUAD, lane c computing column c
+// of every AES (dpf_device.h quad::), so one path walk runs ~2x faster than
+// on one lane when the launch is far below a wave per SIMD.
+template <int BITS>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_quad_kernel(PointParams p) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const quad::Keys kl = quad::keys_of(p.rkl), kd = quad::keys_of(p.rkd), kv = quad::keys_of(p.rkv);
+  const int L = p.num_levels;
+  const int64_t P = p.points_per_key;
+  const int c = quad::column();
+  const uint32_t bmask = (1u << p.bib) - 1u;
+  // The stride is a multiple of 64, so the four lanes of a quad stay together.
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (g >> 2) < p.num_items;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = g >> 2;  // item = key k, point q
+    const int64_t k = u / P, q = u - k * P;
+    const int64_t pi = p.shared_points ? q : u;
+    const Block4 path = load_block(p.tree_index + pi);
+    const int bi = p.block_index ? p.block_index[pi] : (int)(path.w0 & bmask);
+    const int party = p.party[k] & 1;
+    uint32_t s, t;
+    if (p.seeds_in) {
+      s = reinterpret_cast<const uint32_t*>(p.seeds_in + u)[c];
+      t = p.ctrl_in[u] & 1u;
+    } else {
+      s = reinterpret_cast<const uint32_t*>(p.key_seed + k)[c];
+      t = (uint32_t)party;
+    }
+    const dpf_block* cws = p.cw_seed + k * p.cw_stride;
+    const uint8_t* cl = p.cw_left + k * p.cw_stride;
+    const uint8_t* cr = p.cw_right + k * p.cw_stride;
+    for (int j = 0; j < L; ++j) {
+      const uint32_t bit = path_bit(path, L - 1 - j + p.bib);
+      const uint32_t cs = reinterpret_cast<const uint32_t*>(cws + j)[c];
+      const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
+      quad::path_step(lk, kl, kd, s, t, bit, cs, cctl);
+    }
+    const Block4 h = quad::gather(quad::mmo(s, lk, kv, kv, 0u));
+    if (c == 0) {
+      const dpf_block* vcw = p.vcw + k * p.vcw_stride;
+      store_bits<BITS>(p.out + u * (int64_t)p.esz,
+                       fast_point_value<BITS>(h, t, bi, dpf_u128(vcw[bi]), party, p.xor_mode));
+    }
+  }
+}
+
+// DPF_POINTS_QUAD=0 (read per launch) turns the latency mode off (A/B hook).
+bool points_quad_on() {
+  const char* v = std::getenv("DPF_POINTS_QUAD");
+  return !(v && v[0] == '0');
+}
+
 // DPF_POINTS_ILP=2|4 (read per launch) forces two or four chains per lane
 // (four only where a quarter of a key's points is a whole number of waves);
 // by default integer leaves take four chains when the launch fills every CU
@@ -830,6 +886,18 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
     }
   }
   if constexpr (!SUM) {
+    // At most a wave per CU of points: latency-bound, one lane quad per point.
+    const int64_t points = pp.num_keys * pp.points_per_key;
+    if (FAST && points <= (int64_t)num_cus() * 64 && points_ilp() == 0 && points_quad_on()) {
+      g_last_points_kernel = "points/quad";
+      PointParams p = pp;
+      p.num_items = points;
+      const int blk = block_for(points * 4);
+      hipLaunchKernelGGL((eval_points_quad_kernel<BITS>), dim3(grid_for(points * 4, blk)),
+                         dim3(blk), 0, s, p);
+      HIP_TRY(hipGetLastError());
+      return kOk;
+    }
     // Fewer paired items than one wave per CU: latency-bound, run unpaired.
     if (pp.num_items < (int64_t)num_cus() * 64 && points_ilp() != 2) {
       g_last_points_kernel = "points/single";

@@ -251,3 +251,45 @@ def test_points_kernel_default_dispatch():
     dpf.evaluate_at_batch_to_device(sub, 0, _dev_points(pts[:256]), 256, small, shared_points=True)
     torch.cuda.synchronize()
     assert H.last_points_kernel() == "points/ilp2"
+
+
+QUAD_CASES = [
+    ([(128, ("int", 64), 0)], 3, 100),
+    ([(56, ("xor", 128), 0)], 2, 333),
+    ([(40, ("int", 128), 0)], 5, 64),
+    ([(30, ("int", 8), 0)], 4, 77),                  # 16 elements per block
+    ([(10, ("int", 16), 0), (50, ("int", 32), 0)], 3, 50),
+    ([(20, ("int", 64), 0)], 1, 1),
+]
+
+
+@pytest.mark.parametrize("quad", ["1", "0"])
+@pytest.mark.parametrize("levels,n_keys,ppk", QUAD_CASES, ids=str)
+def test_points_latency_mode(levels, n_keys, ppk, quad, monkeypatch):
+    """Small integer point evaluations (at most a wave of points per CU) run
+    one (key, point) per lane quad, lane c computing AES column c
+    (eval_points_quad_kernel); DPF_POINTS_QUAD=0 keeps one chain per lane.
+    Per-key and shared points equal the oracle either way."""
+    import torch
+    from distributed_point_functions_amd import hip_abi as H
+    monkeypatch.setenv("DPF_POINTS_QUAD", quad)
+    h = len(levels) - 1
+    dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=ppk + 17)
+    dev_batch = dpf.upload_key_batch(batch)
+    size = dpf.packed_size(h)
+    pts = _rand_u128(rng, n_keys * ppk, levels[h][0])
+    out = torch.empty(n_keys * ppk * size, dtype=torch.uint8, device="cuda")
+    dpf.evaluate_at_batch_to_device(dev_batch, h, _dev_points(pts), ppk, out)
+    torch.cuda.synchronize()
+    assert H.last_points_kernel() == ("points/quad" if quad == "1" else "points/single")
+    got = out.cpu().numpy().reshape(n_keys * ppk, size)
+    for k in range(n_keys):
+        np.testing.assert_array_equal(got[k * ppk:(k + 1) * ppk],
+                                      O.evaluate_at(P, oks[k], h, pts[k * ppk:(k + 1) * ppk]),
+                                      err_msg=f"key {k}")
+    shared = pts[:ppk]
+    dpf.evaluate_at_batch_to_device(dev_batch, h, _dev_points(shared), ppk, out, shared_points=True)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().reshape(n_keys, ppk, size)
+    for k in range(n_keys):
+        np.testing.assert_array_equal(got[k], O.evaluate_at(P, oks[k], h, shared))
