@@ -290,8 +290,88 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_fast_kernel(DcfFast
   }
 }
 
+// Latency mode of dcf_fast_kernel (small calls: BM_EvaluateDcf evaluates one
+// x per call): one (key, x) per lane QUAD, lane c computing AES column c of
+// the level's value hash and path step together (dpf_device.h quad::).
+template <int BITS, bool XOR>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_fast_quad_kernel(DcfFastParams p,
+                                                                              DcfVcw vc) {
+  __shared__ LdsImage lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const LdsLookup lk = make_lookup(lds);
+  const quad::Keys kl = quad::keys_of(p.rkl), kd = quad::keys_of(p.rkd), kv = quad::keys_of(p.rkv);
+  const int n = p.n;
+  const int c = quad::column();
+  using Acc = typename std::conditional<BITS == 128, u128, uint64_t>::type;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (g >> 2) < p.num_items;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t u = g >> 2;
+    const int64_t k = u / p.points_per_key;
+    const Block4 x = load_block(p.points + (p.shared_points ? u - k * p.points_per_key : u));
+    const uint32_t party = p.party[k] & 1u;
+    uint32_t s = reinterpret_cast<const uint32_t*>(p.key_seed + k)[c];
+    uint32_t t = party;
+    Acc acc = 0;
+    for (int d = 0; d < n; ++d) {
+      const int64_t row = k * p.cw_stride + d;
+      const int pos = n - 1 - d;  // bit of x deciding level d's sum and the next step
+      const uint32_t xb = path_bit(x, pos), pb = n < 128 ? xb : 0u;
+      const uint32_t sg = quad::sigma(s);
+      uint32_t hv = sg, hn = sg;
+      if (d + 1 < n)
+        quad::encrypt2(hv, hn, lk, kv, kl, kd, 0u - pb);
+      else
+        hv = quad::encrypt(hv, lk, kv, kv, 0u);
+      hv ^= sg;
+      hn ^= sg;
+      // Level d's value: element 0 of the value hash, corrected if t, summed
+      // iff bit pos of x is 0 (lane 0 holds the quad's columns in order).
+      const Block4 h = quad::gather(hv);
+      const dpf_block cvb = vc.level[d][k * p.vcw_stride];
+      Acc v, cv;
+      if constexpr (BITS == 128) {
+        v = block_u128(h);
+        cv = dpf_u128(cvb);
+      } else {
+        v = ((uint64_t)h.w1 << 32) | h.w0;
+        cv = cvb.low;
+      }
+      const Acc tc = t ? cv : (Acc)0;
+      const Acc take = xb ? (Acc)0 : ~(Acc)0;
+      if constexpr (XOR) acc ^= (v ^ tc) & take;
+      else acc += (v + tc) & take;
+      if (d + 1 < n) {  // step to node d + 1 (distributed_point_function.cc:323-343)
+        const uint32_t cs = reinterpret_cast<const uint32_t*>(p.cw_seed + row)[c];
+        const uint32_t cc = (uint32_t)(p.cw_left[row] & 1) | ((uint32_t)(p.cw_right[row] & 1) << 1);
+        hn ^= cs & (0u - t);
+        const uint32_t nt = (quad::from_lane0(hn) & 1u) ^ (t & ((cc >> pb) & 1u));
+        if (c == 0) hn &= ~1u;
+        s = hn;
+        t = nt;
+      }
+    }
+    if (c == 0) {
+      if (!XOR && party) acc = (Acc)0 - acc;
+      store_bits<BITS>(p.out + u * (int64_t)p.esz, (u128)acc);
+    }
+  }
+}
+
+// DPF_DCF_QUAD=0 (read per launch) turns the latency mode off (A/B hook).
+bool dcf_quad_on() {
+  const char* v = getenv("DPF_DCF_QUAD");
+  return !(v && v[0] == '0');
+}
+
 template <int BITS, bool XOR>
 void launch_dcf_fast(const DcfFastParams& p0, const DcfVcw& vc, hipStream_t s) {
+  if (p0.num_items <= (int64_t)num_cus() * 64 && dcf_quad_on()) {
+    const int blk = block_for(p0.num_items * 4);
+    hipLaunchKernelGGL((dcf_fast_quad_kernel<BITS, XOR>), dim3(grid_for(p0.num_items * 4, blk)),
+                       dim3(blk), 0, s, p0, vc);
+    return;
+  }
   // One (key, x) pair per lane: two pairs (ILP4, 119-123 VGPRs) measured
   // 11% slower at the bench size (profiles/r13_ab.txt).
   DcfFastParams p = p0;

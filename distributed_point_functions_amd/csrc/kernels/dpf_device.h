@@ -959,6 +959,36 @@ __device__ __forceinline__ void path_step(const LdsLookup& lk, const Keys& left,
   s = h;
   t = nt;
 }
+// Two chains of the quad interleaved round by round: `a` with keys ka, `b`
+// with kb ^ (mask & kd) (DCF: a level's value hash beside its path step).
+__device__ __forceinline__ void encrypt2(uint32_t& a, uint32_t& b, const LdsLookup& lk,
+                                         const Keys& ka, const Keys& kb, const Keys& kd,
+                                         uint32_t mask) {
+  a ^= ka.k[0];
+  b ^= kb.k[0] ^ (mask & kd.k[0]);
+#pragma unroll
+  for (int r = 1; r < 10; ++r) {
+    const uint32_t a1 = from_next<1>(a), a2 = from_next<2>(a), a3 = from_next<3>(a);
+    const uint32_t b1 = from_next<1>(b), b2 = from_next<2>(b), b3 = from_next<3>(b);
+    const uint32_t na = lk.xor3(lk.template lookup<0, 0>(a), lk.template lookup<1, 1>(a1),
+                                lk.template lookup<2, 2>(a2));
+    const uint32_t nb = lk.xor3(lk.template lookup<0, 0>(b), lk.template lookup<1, 1>(b1),
+                                lk.template lookup<2, 2>(b2));
+    a = lk.xor3(na, lk.template lookup<3, 3>(a3), ka.k[r]);
+    b = __builtin_amdgcn_bitop3_b32(lk.xor3(nb, lk.template lookup<3, 3>(b3), kb.k[r]), mask,
+                                    kd.k[r], 0x78);
+  }
+  auto last = [&](uint32_t w, uint32_t k) {
+    const uint32_t w1 = from_next<1>(w), w2 = from_next<2>(w), w3 = from_next<3>(w);
+    const uint32_t x = lk.template lookup<2, 0>(w), y = lk.template lookup<3, 1>(w1);
+    const uint32_t z = lk.template lookup<0, 2>(w2), u = lk.template lookup<1, 3>(w3);
+    const uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
+    const uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
+    return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ k;
+  };
+  a = last(a, ka.k[10]);
+  b = last(b, kb.k[10] ^ (mask & kd.k[10]));
+}
 // The quad's four columns in every lane, as a block (lane 0: in order).
 __device__ __forceinline__ Block4 gather(uint32_t w) {
   return Block4{w, from_next<1>(w), from_next<2>(w), from_next<3>(w)};

@@ -143,12 +143,16 @@ FAST_TYPES = [("int", 8), ("int", 16), ("int", 32), ("int", 64), ("int", 128), (
               ("xor", 64)]
 
 
+@pytest.mark.parametrize("quad", ["1", "0"])
 @pytest.mark.parametrize("vt", FAST_TYPES, ids=str)
 @pytest.mark.parametrize("n,shared", [(17, False), (64, True), (128, False)], ids=str)
-def test_dcf_fast_kernel_uniform_keys(vt, n, shared, monkeypatch):
+def test_dcf_fast_kernel_uniform_keys(vt, n, shared, quad, monkeypatch):
     """dcf_fast_kernel with wave-uniform keys (points_per_key % 64 == 0) is
     bit-exact against the general kernel on every output and against the
-    oracle on sampled rows."""
+    oracle on sampled rows -- in latency mode (a launch this small runs one
+    (key, x) per lane quad, dcf_fast_quad_kernel) and, with DPF_DCF_QUAD=0,
+    one per lane."""
+    monkeypatch.setenv("DPF_DCF_QUAD", quad)
     nk, ppk = 24, 128
     dcf, P, beta, alphas, pts, run = _batch_case(vt, n, nk, ppk, shared, seed=n * 7 + len(vt))
     got = run()
