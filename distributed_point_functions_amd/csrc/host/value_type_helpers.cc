@@ -393,6 +393,18 @@ void AdviseHugePages(void* p, size_t bytes) {
   if (hi > lo) (void)madvise(reinterpret_cast<void*>(lo), hi - lo, MADV_HUGEPAGE);
 }
 
+const void* ZeroPages(size_t* bytes) {
+  constexpr size_t kSpan = size_t{64} << 20;
+  // Never written: every page reads as the kernel's shared zero page, so a
+  // memmove out of it reads from cache.  Null (and resize()) if mmap fails.
+  static const void* const zeros = [] {
+    void* p = mmap(nullptr, kSpan, PROT_READ, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    return p == MAP_FAILED ? static_cast<const void*>(nullptr) : static_cast<const void*>(p);
+  }();
+  *bytes = zeros ? kSpan : 0;
+  return zeros;
+}
+
 void PrefaultPages(void* p, size_t bytes) {
   if (!p || bytes < (size_t{64} << 20)) return;
   constexpr size_t kPage = 4096;

@@ -278,6 +278,34 @@ void ReserveOutputVector(std::vector<T>& out, int64_t n, bool prefault = true) {
   if (prefault) PrefaultPages(out.data(), static_cast<size_t>(n) * sizeof(T));
 }
 
+// A read-only mapping of `*bytes` (64 MiB) bytes of the kernel's zero page,
+// made on first use and kept for the life of the process.
+const void* ZeroPages(size_t* bytes);
+
+// out->resize(n) for a growing vector, with the value-initialisation of
+// integer elements (absl::uint128 included) done by memmove from ZeroPages():
+// libstdc++ value-initialises a 16-byte element with a load/store loop (34
+// GB/s on the GPU box's host) where a large memmove or memset streams at 70-75
+// GB/s -- the one-thread bound of config 3's 32 GiB host output
+// (profiles/r15_value_init_probe.jsonl).  Other element types: resize().
+template <typename T>
+void GrowZeroed(std::vector<T>* out, size_t n) {
+  if constexpr (std::is_arithmetic_v<T> || std::is_same_v<T, uint128>) {
+    size_t span = 0;
+    const T* zeros = static_cast<const T*>(ZeroPages(&span));
+    const size_t per = span / sizeof(T);
+    if (zeros && per > 0) {
+      while (out->size() < n) {
+        const size_t k = n - out->size() < per ? n - out->size() : per;
+        out->insert(out->end(), zeros, zeros + k);
+      }
+      if (out->size() > n) out->resize(n);
+      return;
+    }
+  }
+  out->resize(n);
+}
+
 // A value-initialised std::vector<T> of n elements whose storage was advised
 // onto huge pages and mapped on the host threads before the (one-thread)
 // initialisation touched it.
@@ -285,7 +313,7 @@ template <typename T>
 std::vector<T> MakeOutputVector(int64_t n) {
   std::vector<T> out;
   ReserveOutputVector(out, n);
-  out.resize(n);
+  GrowZeroed(&out, static_cast<size_t>(n));
   return out;
 }
 
@@ -317,9 +345,9 @@ HostSink VectorSink(std::vector<T>* out) {
     ReserveOutputVector(*out, static_cast<int64_t>(bytes / sizeof(T)), false);
     return out->data();
   };
-  s.grow = [out](size_t bytes) { out->resize((bytes + sizeof(T) - 1) / sizeof(T)); };
+  s.grow = [out](size_t bytes) { GrowZeroed(out, (bytes + sizeof(T) - 1) / sizeof(T)); };
   s.chunk = [out](const uint8_t* src, size_t offset, size_t len) {
-    out->resize((offset + len) / sizeof(T));
+    GrowZeroed(out, (offset + len) / sizeof(T));
     uint8_t* dst = reinterpret_cast<uint8_t*>(out->data()) + offset;
     ParallelRanges(static_cast<int64_t>(len), int64_t{2} << 20, [&](int64_t lo, int64_t hi) {
       std::memcpy(dst + lo, src + lo, static_cast<size_t>(hi - lo));
