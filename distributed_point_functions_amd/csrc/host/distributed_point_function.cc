@@ -793,33 +793,38 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
     return InvalidArgumentError("device output buffer too small");
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
-  // Walk the root to the shard's subtree root along the top k tree bits.
-  dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
-  uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
-  dpf_block path = ToBlock(static_cast<uint128>(shard));
-  DPF_RETURN_IF_ERROR(s->Upload(s->start_seed, &root, 1, stream));
-  DPF_RETURN_IF_ERROR(s->Upload(s->start_ctrl, &party, 1, stream));
-  DPF_RETURN_IF_ERROR(s->Upload(s->paths, &path, 1, stream));
-  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
-  if (k > 0) {
-    DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), 0, k, s, stream));
-    HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(1, k, s->start_seed.as<dpf_block>(),
-                                           s->start_ctrl.as<uint8_t>(), s->paths.as<dpf_block>(),
-                                           s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
-                                           s->cw_right.as<uint8_t>(), &kl, &kr,
-                                           s->start_seed.as<dpf_block>(),
-                                           s->start_ctrl.as<uint8_t>(), stream));
-  }
+  // Everything the launches read -- root, party, shard path, value correction
+  // and both correction-word ranges -- goes up as ONE page-locked image and
+  // one async H2D (seven synchronous uploads had cost ~30 us per call, as
+  // much as config 1's whole expansion kernel).
+  const dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+  const uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
+  const dpf_block path = ToBlock(static_cast<uint128>(shard));
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  DPF_RETURN_IF_ERROR(s->Upload(s->vcw, vcw_blocks.data(), vcw_blocks.size(), stream));
-  DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), k, stop_level, s, stream));
+  PackedUploads& up = s->packed;
+  DPF_RETURN_IF_ERROR(up.Reset());
+  const size_t o_seed = up.Add(&root, 1), o_ctrl = up.Add(&party, 1), o_path = up.Add(&path, 1);
+  const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());
+  const PackedCws o_top = AddCorrectionWords(ctx.key(), 0, k, up);
+  const PackedCws o_cw = AddCorrectionWords(ctx.key(), k, stop_level, up);
+  DPF_RETURN_IF_ERROR(up.Commit(stream));
+  dpf_block* seed = up.Ptr<dpf_block>(o_seed);
+  uint8_t* ctrl = up.Ptr<uint8_t>(o_ctrl);
+  const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
+  if (k > 0) {
+    // Walk the root to the shard's subtree root along the top k tree bits (in place).
+    HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(1, k, seed, ctrl, up.Ptr<dpf_block>(o_path),
+                                           up.Ptr<dpf_block>(o_top.seed), up.Ptr<uint8_t>(o_top.left),
+                                           up.Ptr<uint8_t>(o_top.right), &kl, &kr, seed, ctrl,
+                                           stream));
+  }
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
-  HIP_RETURN_IF_ERROR(dpf_hip_expand(1, s->start_seed.as<dpf_block>(), s->start_ctrl.as<uint8_t>(),
-                                     stop_level - k, s->cw_seed.as<dpf_block>(),
-                                     s->cw_left.as<uint8_t>(), s->cw_right.as<uint8_t>(), &kl, &kr,
-                                     &kv, &desc, cepb, s->vcw.as<dpf_block>(), party, device_out,
-                                     stream));
+  HIP_RETURN_IF_ERROR(dpf_hip_expand(1, seed, ctrl, stop_level - k, up.Ptr<dpf_block>(o_cw.seed),
+                                     up.Ptr<uint8_t>(o_cw.left), up.Ptr<uint8_t>(o_cw.right), &kl,
+                                     &kr, &kv, &desc, cepb, up.Ptr<dpf_block>(o_vcw), party,
+                                     device_out, stream));
+  DPF_RETURN_IF_ERROR(up.MarkUsed(stream));
   ctx.set_previous_hierarchy_level(hierarchy_level);
   return total;
 }

@@ -921,25 +921,68 @@ __device__ __forceinline__ uint32_t sigma(uint32_t x) {
   return column() < 2 ? y : (x ^ y);
 }
 
+// DPF_QUAD_LOOKUP_FIRST=1: lane c looks up all four bytes of its OWN column
+// (T0[b0(w_c)], T1[b1(w_c)], T2[b2(w_c)], T3[b3(w_c)]) and the quad permutes
+// the looked-up words instead of the state: n_c = A_c ^ B_c+1 ^ C_c+2 ^ D_c+3.
+// The lookups' addresses then depend on w directly (no DPP move and its
+// wait states ahead of the LDS reads), and the moves fold into the XORs
+// after them.  =0: permute the state, then look up (r15 first version).
+#ifndef DPF_QUAD_LOOKUP_FIRST
+#define DPF_QUAD_LOOKUP_FIRST 1
+#endif
+// from_next for a value the next instruction XORs: bound_ctrl set and no
+// `old` operand, so the compiler can fold the move into that XOR as its DPP
+// source (every lane of a quad_perm is valid, so bound_ctrl changes nothing).
+template <int K>
+__device__ __forceinline__ uint32_t xfrom_next(uint32_t v) {
+  constexpr int ctrl = K == 1 ? (1 | 2 << 2 | 3 << 4 | 0 << 6)
+                       : K == 2 ? (2 | 3 << 2 | 0 << 4 | 1 << 6)
+                                : (3 | 0 << 2 | 1 << 4 | 2 << 6);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xf, 0xf, true);
+}
+// One middle round of column c; k: this column's round-key word.
+__device__ __forceinline__ uint32_t round_mid(uint32_t w, const LdsLookup& lk, uint32_t k) {
+#if DPF_QUAD_LOOKUP_FIRST
+  const uint32_t a = lk.template lookup<0, 0>(w), b = lk.template lookup<1, 1>(w);
+  const uint32_t c = lk.template lookup<2, 2>(w), d = lk.template lookup<3, 3>(w);
+  return ((a ^ k) ^ xfrom_next<1>(b)) ^ xfrom_next<2>(c) ^ xfrom_next<3>(d);
+#else
+  const uint32_t b = from_next<1>(w), c = from_next<2>(w), d = from_next<3>(w);
+  return lk.xor3(lk.xor3(lk.template lookup<0, 0>(w), lk.template lookup<1, 1>(b),
+                         lk.template lookup<2, 2>(c)),
+                 lk.template lookup<3, 3>(d), k);
+#endif
+}
+// The last round of column c (SubBytes + ShiftRows), without the round key.
+__device__ __forceinline__ uint32_t round_last(uint32_t w, const LdsLookup& lk) {
+#if DPF_QUAD_LOOKUP_FIRST
+  const uint32_t x = lk.template lookup<2, 0>(w);
+  const uint32_t y = xfrom_next<1>(lk.template lookup<3, 1>(w));
+  const uint32_t z = xfrom_next<2>(lk.template lookup<0, 2>(w));
+  const uint32_t u = xfrom_next<3>(lk.template lookup<1, 3>(w));
+#else
+  const uint32_t b = from_next<1>(w), c = from_next<2>(w), d = from_next<3>(w);
+  const uint32_t x = lk.template lookup<2, 0>(w), y = lk.template lookup<3, 1>(b);
+  const uint32_t z = lk.template lookup<0, 2>(c), u = lk.template lookup<1, 3>(d);
+#endif
+  const uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
+  const uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
+  return (xy & 0x0000ffffu) | (zu & 0xffff0000u);
+}
+
 // AES-128 of the quad's state (this lane: column c); round key word r of
 // this column = left.k[r] ^ (mask & diff.k[r]) (mask 0: left alone).
 __device__ __forceinline__ uint32_t encrypt(uint32_t w, const LdsLookup& lk, const Keys& left,
                                             const Keys& diff, uint32_t mask) {
-  w ^= left.k[0] ^ (mask & diff.k[0]);
+  // The round keys of this chain first (they depend on the mask only), so
+  // each round ends in one XOR.
+  uint32_t k[11];
 #pragma unroll
-  for (int r = 1; r < 10; ++r) {
-    const uint32_t b = from_next<1>(w), c = from_next<2>(w), d = from_next<3>(w);
-    const uint32_t n = lk.xor3(lk.template lookup<0, 0>(w), lk.template lookup<1, 1>(b),
-                               lk.template lookup<2, 2>(c));
-    w = __builtin_amdgcn_bitop3_b32(lk.xor3(n, lk.template lookup<3, 3>(d), left.k[r]), mask,
-                                    diff.k[r], 0x78);
-  }
-  const uint32_t b = from_next<1>(w), c = from_next<2>(w), d = from_next<3>(w);
-  const uint32_t x = lk.template lookup<2, 0>(w), y = lk.template lookup<3, 1>(b);
-  const uint32_t z = lk.template lookup<0, 2>(c), u = lk.template lookup<1, 3>(d);
-  const uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
-  const uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
-  return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ left.k[10] ^ (mask & diff.k[10]);
+  for (int r = 0; r < 11; ++r) k[r] = __builtin_amdgcn_bitop3_b32(left.k[r], mask, diff.k[r], 0x78);
+  w ^= k[0];
+#pragma unroll
+  for (int r = 1; r < 10; ++r) w = round_mid(w, lk, k[r]);
+  return round_last(w, lk) ^ k[10];
 }
 __device__ __forceinline__ uint32_t mmo(uint32_t x, const LdsLookup& lk, const Keys& left,
                                         const Keys& diff, uint32_t mask) {
@@ -964,34 +1007,53 @@ __device__ __forceinline__ void path_step(const LdsLookup& lk, const Keys& left,
 __device__ __forceinline__ void encrypt2(uint32_t& a, uint32_t& b, const LdsLookup& lk,
                                          const Keys& ka, const Keys& kb, const Keys& kd,
                                          uint32_t mask) {
+  uint32_t k[11];
+#pragma unroll
+  for (int r = 0; r < 11; ++r) k[r] = __builtin_amdgcn_bitop3_b32(kb.k[r], mask, kd.k[r], 0x78);
   a ^= ka.k[0];
-  b ^= kb.k[0] ^ (mask & kd.k[0]);
+  b ^= k[0];
 #pragma unroll
   for (int r = 1; r < 10; ++r) {
-    const uint32_t a1 = from_next<1>(a), a2 = from_next<2>(a), a3 = from_next<3>(a);
-    const uint32_t b1 = from_next<1>(b), b2 = from_next<2>(b), b3 = from_next<3>(b);
-    const uint32_t na = lk.xor3(lk.template lookup<0, 0>(a), lk.template lookup<1, 1>(a1),
-                                lk.template lookup<2, 2>(a2));
-    const uint32_t nb = lk.xor3(lk.template lookup<0, 0>(b), lk.template lookup<1, 1>(b1),
-                                lk.template lookup<2, 2>(b2));
-    a = lk.xor3(na, lk.template lookup<3, 3>(a3), ka.k[r]);
-    b = __builtin_amdgcn_bitop3_b32(lk.xor3(nb, lk.template lookup<3, 3>(b3), kb.k[r]), mask,
-                                    kd.k[r], 0x78);
+    const uint32_t na = round_mid(a, lk, ka.k[r]), nb = round_mid(b, lk, k[r]);
+    a = na;
+    b = nb;
   }
-  auto last = [&](uint32_t w, uint32_t k) {
-    const uint32_t w1 = from_next<1>(w), w2 = from_next<2>(w), w3 = from_next<3>(w);
-    const uint32_t x = lk.template lookup<2, 0>(w), y = lk.template lookup<3, 1>(w1);
-    const uint32_t z = lk.template lookup<0, 2>(w2), u = lk.template lookup<1, 3>(w3);
-    const uint32_t xy = (x & 0x000000ffu) | (y & 0xffffff00u);
-    const uint32_t zu = (z & 0x00ff0000u) | (u & 0xff00ffffu);
-    return ((xy & 0x0000ffffu) | (zu & 0xffff0000u)) ^ k;
-  };
-  a = last(a, ka.k[10]);
-  b = last(b, kb.k[10] ^ (mask & kd.k[10]));
+  a = round_last(a, lk) ^ ka.k[10];
+  b = round_last(b, lk) ^ k[10];
 }
 // The quad's four columns in every lane, as a block (lane 0: in order).
 __device__ __forceinline__ Block4 gather(uint32_t w) {
   return Block4{w, from_next<1>(w), from_next<2>(w), from_next<3>(w)};
+}
+// Both children of the quad's node (children_step above, one column per
+// lane): the left and right hashes interleaved round by round.
+__device__ __forceinline__ void children(const LdsLookup& lk, const Keys& left, const Keys& diff,
+                                         uint32_t s, uint32_t t, uint32_t cs, uint32_t cctl,
+                                         uint32_t& c0, uint32_t& t0, uint32_t& c1, uint32_t& t1) {
+  const uint32_t x = sigma(s);
+  uint32_t a = x, b = x;
+  encrypt2(a, b, lk, left, left, diff, ~0u);
+  const uint32_t m = cs & (0u - t);
+  a ^= x ^ m;
+  b ^= x ^ m;
+  t0 = (from_lane0(a) & 1u) ^ (t & (cctl & 1u));
+  t1 = (from_lane0(b) & 1u) ^ (t & ((cctl >> 1) & 1u));
+  if (column() == 0) {
+    a &= ~1u;
+    b &= ~1u;
+  }
+  c0 = a;
+  c1 = b;
+}
+// The value hashes of two seeds (mmo with the value key), interleaved.
+__device__ __forceinline__ void hash2(const LdsLookup& lk, const Keys& value, uint32_t& a,
+                                      uint32_t& b) {
+  const uint32_t xa = sigma(a), xb = sigma(b);
+  a = xa;
+  b = xb;
+  encrypt2(a, b, lk, value, value, value, 0u);
+  a ^= xa;
+  b ^= xb;
 }
 }  // namespace quad
 

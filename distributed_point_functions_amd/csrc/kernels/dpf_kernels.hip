@@ -410,6 +410,117 @@ struct PointParams {
   RoundKeys rkl, rkd, rkv;
 };
 
+// Latency mode of full-domain expansion for small trees (r15; config 1 and
+// the reference's BM_EvaluateRegularDpf below ~2^20 outputs).  expand_kernel /
+// the octet kernel give every lane its own subtree and walk each one from the
+// start seed: at 2^19 leaves that is 262144 walks of 18 levels, 3.7x the
+// algorithmic AES, and each lane's chain is latency-bound.  Here workgroup w
+// owns the subtree at depth t = p.k0 under start w >> t (one workgroup per CU
+// at most) and expands its D = p.S levels breadth-first through LDS, so every
+// node is hashed once:
+//   * wave 0 walks the t levels to the subtree root, one chain per lane QUAD
+//     (quad::path_step);
+//   * a level of <= 256 parents: quad q expands parent q into both children
+//     (quad::children, the two hashes interleaved);
+//   * a wider level: lane i expands parent i (children_step, ILP2);
+//   * level D: lane (or quad) i expands parent i and value-hashes its two
+//     leaves, which are stored side by side at (w << D) + 2i.
+// Nodes live in nodes[] / tbits[] (<= 1024 per level, so D <= 11), read into
+// registers before a barrier and rewritten after it.
+constexpr int kSmallMaxD = 11;
+template <int BITS, bool XOR>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_small_kernel(ExpandParams p,
+                                                                            FastIntLeaf<BITS, XOR> leaf) {
+  __shared__ LdsImage lds;
+  __shared__ uint4 nodes[kBlock];
+  __shared__ uint32_t tbits[kBlock];
+  leaf.init();
+  fill_tables(lds.tab);
+  fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  __syncthreads();
+  const LdsLookup lk =
+      make_lookup(lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
+  const quad::Keys ql = quad::keys_of(p.rkl), qd = quad::keys_of(p.rkd);
+  const int t = p.k0, D = p.S;
+  const int64_t w = blockIdx.x;
+  const int tid = threadIdx.x, c = quad::column(), q = tid >> 2;
+  auto word = [](const uint4& v, int i) { return reinterpret_cast<const uint32_t*>(&v)[i]; };
+  if (tid < 64) {
+    const int64_t r = w >> t;
+    uint32_t s = reinterpret_cast<const uint32_t*>(p.seeds_in + r)[c];
+    uint32_t tt = p.ctrl_in[r] & 1u;
+    for (int j = 0; j < t; ++j) {
+      const uint32_t bit = (uint32_t)((w >> (t - 1 - j)) & 1);
+      quad::path_step(lk, ql, qd, s, tt, bit, word(lds.cw_seed[j], c), lds.cw_ctrl[j]);
+    }
+    if (tid < 4) {
+      reinterpret_cast<uint32_t*>(&nodes[0])[c] = s;
+      if (c == 0) tbits[0] = tt;
+    }
+  }
+  __syncthreads();
+  for (int j = 1; j < D; ++j) {
+    const int lvl = t + j - 1, npar = 1 << (j - 1);
+    if (npar <= kBlock / 4) {
+      const bool on = q < npar;
+      uint32_t c0 = 0, c1 = 0, t0 = 0, t1 = 0;
+      if (on)
+        quad::children(lk, ql, qd, word(nodes[q], c), tbits[q], word(lds.cw_seed[lvl], c),
+                       lds.cw_ctrl[lvl], c0, t0, c1, t1);
+      __syncthreads();
+      if (on) {
+        reinterpret_cast<uint32_t*>(&nodes[2 * q])[c] = c0;
+        reinterpret_cast<uint32_t*>(&nodes[2 * q + 1])[c] = c1;
+        if (c == 0) {
+          tbits[2 * q] = t0;
+          tbits[2 * q + 1] = t1;
+        }
+      }
+      __syncthreads();
+    } else {
+      const bool on = tid < npar;
+      Block4 c0{}, c1{};
+      uint32_t t0 = 0, t1 = 0;
+      if (on) {
+        const uint4 v = nodes[tid];
+        children_step(lk, lk.ks.l, lk.ks.r, Block4{v.x, v.y, v.z, v.w}, tbits[tid],
+                      lds.cw_seed[lvl], lds.cw_ctrl[lvl], c0, t0, c1, t1);
+      }
+      __syncthreads();
+      if (on) {
+        nodes[2 * tid] = make_uint4(c0.w0, c0.w1, c0.w2, c0.w3);
+        nodes[2 * tid + 1] = make_uint4(c1.w0, c1.w1, c1.w2, c1.w3);
+        tbits[2 * tid] = t0;
+        tbits[2 * tid + 1] = t1;
+      }
+      __syncthreads();
+    }
+  }
+  const int lvl = t + D - 1, npar = 1 << (D - 1);
+  const int64_t leaf0 = w << D;
+  if (npar <= kBlock / 4) {
+    if (q < npar) {
+      const quad::Keys qv = quad::keys_of(p.rkv);
+      uint32_t c0, c1, t0, t1;
+      quad::children(lk, ql, qd, word(nodes[q], c), tbits[q], word(lds.cw_seed[lvl], c),
+                     lds.cw_ctrl[lvl], c0, t0, c1, t1);
+      quad::hash2(lk, qv, c0, c1);
+      const Block4 h0 = quad::gather(c0), h1 = quad::gather(c1);
+      if (c == 0) {
+        leaf.store(leaf.correct(h0, t0), leaf0 + 2 * q, p.out);
+        leaf.store(leaf.correct(h1, t1), leaf0 + 2 * q + 1, p.out);
+      }
+    }
+  } else if (tid < npar) {
+    const uint4 v = nodes[tid];
+    Block4 c0, c1;
+    uint32_t t0, t1;
+    children_step(lk, lk.ks.l, lk.ks.r, Block4{v.x, v.y, v.z, v.w}, tbits[tid], lds.cw_seed[lvl],
+                  lds.cw_ctrl[lvl], c0, t0, c1, t1);
+    leaf.emit2(lk, lk.ks.v, c0, t0, c1, t1, leaf0 + 2 * tid, p.out);
+  }
+}
+
 // PAIRED = false (launches below one wave per CU, never in sum mode): one
 // chain per lane, half = P, so a small call spreads over twice the CUs and each
 // wave's dependent AES chain issues half the LDS reads per round.
@@ -684,9 +795,51 @@ bool launch_octet(const ExpandParams& p, const dpf_block* vcw, int E, int party,
   return true;
 }
 
+// Latency mode for small trees (expand_small_kernel): num_starts << t
+// workgroups, t as large as keeps them within one per CU, and D = L - t
+// levels breadth-first in each; D must be 1..kSmallMaxD.  Returns false (and
+// launches nothing) when the tree does not fit that shape.  DPF_EXPAND_SMALL=0
+// (read per launch) turns it off: the A/B and test hook.
+bool small_on() {
+  const char* v = std::getenv("DPF_EXPAND_SMALL");
+  return !(v && v[0] == '0');
+}
+bool small_shape(int64_t num_starts, int num_levels, int* t, int* D) {
+  const int64_t cus = num_cus();
+  if (!small_on() || num_levels < 1 || num_starts < 1 || num_starts > cus) return false;
+  int tt = 0;
+  while (tt < num_levels - 1 && (num_starts << (tt + 1)) <= cus) ++tt;
+  const int d = num_levels - tt;
+  if (d < 1 || d > kSmallMaxD) return false;
+  *t = tt;
+  *D = d;
+  return true;
+}
+template <int BITS, bool XOR>
+int launch_small(const ExpandParams& p0, int64_t num_starts, int t, int D, const dpf_block* vcw,
+                 int E, int party, int store_bytes, hipStream_t s) {
+  ExpandParams p = p0;
+  p.k0 = t;
+  p.S = D;
+  p.num_items = num_starts << t;
+  static const std::string name = std::string("small/") + leaf_name<FastIntLeaf<BITS, XOR>>();
+  g_last_expand = name.c_str();
+  g_last_expand_s = D;
+  hipLaunchKernelGGL((expand_small_kernel<BITS, XOR>), dim3((unsigned)p.num_items), dim3(kBlock), 0,
+                     s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
+  HIP_TRY(hipGetLastError());
+  return kOk;
+}
+
 template <int BITS>
 int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf_block* vcw,
                        int E, int party, int store_bytes, hipStream_t s) {
+  int t = 0, D = 0;
+  const int64_t starts = p.num_items >> p.k0;
+  if (small_shape(starts, p.num_levels, &t, &D))
+    return d->kind[0] == DPF_LEAF_XOR
+               ? launch_small<BITS, true>(p, starts, t, D, vcw, E, party, store_bytes, s)
+               : launch_small<BITS, false>(p, starts, t, D, vcw, E, party, store_bytes, s);
   if (d->kind[0] == DPF_LEAF_XOR ? launch_octet<BITS, true>(p, vcw, E, party, store_bytes, s)
                                  : launch_octet<BITS, false>(p, vcw, E, party, store_bytes, s)) {
     HIP_TRY(hipGetLastError());
@@ -1567,10 +1720,23 @@ int dpf_hip_memcpy_d2h_staged_after(void* dst, const void* src, size_t bytes,
         if (rc != kNoHelperThread) return rc;
         // No helper thread: map and register the whole range first.
       }
+      using clk = std::chrono::steady_clock;
+      const auto t0 = clk::now();
       prefault((char*)dst, bytes, 16);
-      if (acquire_host(dst, bytes, false, &base) == kAcquired)
-        return registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true,
-                               before_chunk, ctx, (hipStream_t)stream, base);
+      const auto t1 = clk::now();
+      if (acquire_host(dst, bytes, false, &base) == kAcquired) {
+        const auto t2 = clk::now();
+        const int rc = registered_copy((char*)dst, (char*)const_cast<void*>(src), bytes, true,
+                                       before_chunk, ctx, (hipStream_t)stream, base);
+        if (std::getenv("DPF_HIP_D2H_TRACE"))
+          fprintf(stderr, "[whole_d2h] %zu MiB: total %.1f ms, map %.1f ms, register %.1f ms, "
+                  "copy+unregister %.1f ms\n", bytes >> 20,
+                  1e3 * std::chrono::duration<double>(clk::now() - t0).count(),
+                  1e3 * std::chrono::duration<double>(t1 - t0).count(),
+                  1e3 * std::chrono::duration<double>(t2 - t1).count(),
+                  1e3 * std::chrono::duration<double>(clk::now() - t2).count());
+        return rc;
+      }
     }
   }
   before_chunk(ctx, bytes);

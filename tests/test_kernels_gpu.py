@@ -214,6 +214,29 @@ def test_expand_specialised_leaves_octet(hip, i, party, levels, n0, monkeypatch)
         assert hip.last_expand_kernel()[0] == "pair/" + want[6:]
 
 
+# Small trees (<= one workgroup per CU, <= 11 levels below the workgroups'
+# subtree roots) run expand_small_kernel: wave 0 walks to the subtree root
+# in quads, the levels are expanded breadth-first through LDS (quads while a
+# level has <= 256 parents, lanes above), the last level's two leaves per
+# parent hashed side by side.  Every shape -- config 1's (one start, 19
+# levels: 256 workgroups of 11 levels), one workgroup, several starts, leaves
+# narrower than a block -- matches the oracle, reports "small/fast", and
+# equals the general launch (DPF_EXPAND_SMALL=0) byte for byte.
+@pytest.mark.parametrize("vt,levels,n0,cepb", [
+    (("int", 64), 19, 1, None), (("xor", 128), 19, 1, None), (("int", 64), 11, 1, None),
+    (("int", 32), 12, 3, None), (("int", 128), 8, 256, None), (("int", 8), 10, 2, 4),
+    (("xor", 16), 1, 1, None), (("int", 64), 9, 200, 1)], ids=str)
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_small_trees(hip, vt, levels, n0, cepb, party, monkeypatch):
+    seed = hash((str(vt), levels, n0, cepb, party, "small")) & 0xFFFFFFFF
+    _expand_case(hip, np.random.default_rng(seed), vt, n0, levels, party, cepb=cepb)
+    name, depth = hip.last_expand_kernel()
+    assert name == "small/fast" and 1 <= depth <= 11, (name, depth)
+    monkeypatch.setenv("DPF_EXPAND_SMALL", "0")
+    _expand_case(hip, np.random.default_rng(seed), vt, n0, levels, party, cepb=cepb)
+    assert not hip.last_expand_kernel()[0].startswith("small/")
+
+
 # Start counts that are not powers of two: dpf_hip_expand picks the subtree
 # depth by the per-thread critical path (5 starts x 2^21: depth 4, 5 * 2^17
 # subtrees in 3 even rounds, where "fill the launch" gave depth 5 in 2 rounds).
