@@ -423,14 +423,16 @@ struct PointParams {
 //   * a level of <= 256 parents: quad q expands parent q into both children
 //     (quad::children, the two hashes interleaved);
 //   * a wider level: lane i expands parent i (children_step, ILP2);
-//   * level D: lane (or quad) i expands parent i and value-hashes its two
-//     leaves, which are stored side by side at (w << D) + 2i.
+//   * level D: lane i expands parent i and value-hashes its two leaves
+//     (Leaf::emit2), stored side by side at (w << D) + 2i; integer leaves of
+//     a level of <= 256 parents do that in quads.
 // Nodes live in nodes[] / tbits[] (<= 1024 per level, so D <= 11), read into
 // registers before a barrier and rewritten after it.
 constexpr int kSmallMaxD = 11;
-template <int BITS, bool XOR>
-__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_small_kernel(ExpandParams p,
-                                                                            FastIntLeaf<BITS, XOR> leaf) {
+template <class Leaf> struct IsFastInt : std::false_type {};
+template <int BITS, bool XOR> struct IsFastInt<FastIntLeaf<BITS, XOR>> : std::true_type {};
+template <class Leaf>
+__global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_small_kernel(ExpandParams p, Leaf leaf) {
   __shared__ LdsImage lds;
   __shared__ uint4 nodes[kBlock];
   __shared__ uint32_t tbits[kBlock];
@@ -498,8 +500,10 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_small_kernel(Exp
   }
   const int lvl = t + D - 1, npar = 1 << (D - 1);
   const int64_t leaf0 = w << D;
-  if (npar <= kBlock / 4) {
-    if (q < npar) {
+  bool quad_last = false;
+  if constexpr (IsFastInt<Leaf>::value) quad_last = npar <= kBlock / 4;
+  if (quad_last) {
+    if constexpr (IsFastInt<Leaf>::value) if (q < npar) {
       const quad::Keys qv = quad::keys_of(p.rkv);
       uint32_t c0, c1, t0, t1;
       quad::children(lk, ql, qd, word(nodes[q], c), tbits[q], word(lds.cw_seed[lvl], c),
@@ -771,8 +775,52 @@ void note_expand(const ExpandParams& p, bool octet) {
   g_last_expand_s = p.S;
 }
 
+// Latency mode for small trees (expand_small_kernel): num_starts << t
+// workgroups, t as large as keeps them within one per CU, and D = L - t
+// levels breadth-first in each; D must be 1..kSmallMaxD.  Returns false (and
+// launches nothing) when the tree does not fit that shape.  DPF_EXPAND_SMALL=0
+// (read per launch) turns it off: the A/B and test hook.
+bool small_on() {
+  const char* v = std::getenv("DPF_EXPAND_SMALL");
+  return !(v && v[0] == '0');
+}
+bool small_shape(int64_t num_starts, int num_levels, int* t, int* D) {
+  const int64_t cus = num_cus();
+  if (!small_on() || num_levels < 1 || num_starts < 1 || num_starts > cus) return false;
+  int tt = 0;
+  while (tt < num_levels - 1 && (num_starts << (tt + 1)) <= cus) ++tt;
+  const int d = num_levels - tt;
+  if (d < 1 || d > kSmallMaxD) return false;
+  *t = tt;
+  *D = d;
+  return true;
+}
+// Launches expand_small_kernel<Leaf> when the tree has the small shape.
+template <class Leaf>
+bool try_small(const ExpandParams& p0, const Leaf& leaf, hipStream_t s) {
+  int t = 0, D = 0;
+  const int64_t starts = p0.num_items >> p0.k0;
+  if (!small_shape(starts, p0.num_levels, &t, &D)) return false;
+  ExpandParams p = p0;
+  p.k0 = t;
+  p.S = D;
+  p.num_items = starts << t;
+  static const std::string name = std::string("small/") + leaf_name<Leaf>();
+  g_last_expand = name.c_str();
+  g_last_expand_s = D;
+  hipLaunchKernelGGL((expand_small_kernel<Leaf>), dim3((unsigned)p.num_items), dim3(kBlock), 0, s,
+                     p, leaf);
+  return true;
+}
+
 template <class Leaf>
 int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
+  // GenericLeaf's conversion spills in the small kernel's register budget and
+  // measured 0.93-1.07x there (profiles/r15_ab.txt part 13): not dispatched.
+  if (!std::is_same_v<Leaf, GenericLeaf> && try_small(p, leaf, s)) {
+    HIP_TRY(hipGetLastError());
+    return kOk;
+  }
   note_expand<Leaf>(p, false);
   const int blk = block_for(p.num_items);
   hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid_for(p.num_items, blk)), dim3(blk), 0, s, p,
@@ -795,51 +843,14 @@ bool launch_octet(const ExpandParams& p, const dpf_block* vcw, int E, int party,
   return true;
 }
 
-// Latency mode for small trees (expand_small_kernel): num_starts << t
-// workgroups, t as large as keeps them within one per CU, and D = L - t
-// levels breadth-first in each; D must be 1..kSmallMaxD.  Returns false (and
-// launches nothing) when the tree does not fit that shape.  DPF_EXPAND_SMALL=0
-// (read per launch) turns it off: the A/B and test hook.
-bool small_on() {
-  const char* v = std::getenv("DPF_EXPAND_SMALL");
-  return !(v && v[0] == '0');
-}
-bool small_shape(int64_t num_starts, int num_levels, int* t, int* D) {
-  const int64_t cus = num_cus();
-  if (!small_on() || num_levels < 1 || num_starts < 1 || num_starts > cus) return false;
-  int tt = 0;
-  while (tt < num_levels - 1 && (num_starts << (tt + 1)) <= cus) ++tt;
-  const int d = num_levels - tt;
-  if (d < 1 || d > kSmallMaxD) return false;
-  *t = tt;
-  *D = d;
-  return true;
-}
-template <int BITS, bool XOR>
-int launch_small(const ExpandParams& p0, int64_t num_starts, int t, int D, const dpf_block* vcw,
-                 int E, int party, int store_bytes, hipStream_t s) {
-  ExpandParams p = p0;
-  p.k0 = t;
-  p.S = D;
-  p.num_items = num_starts << t;
-  static const std::string name = std::string("small/") + leaf_name<FastIntLeaf<BITS, XOR>>();
-  g_last_expand = name.c_str();
-  g_last_expand_s = D;
-  hipLaunchKernelGGL((expand_small_kernel<BITS, XOR>), dim3((unsigned)p.num_items), dim3(kBlock), 0,
-                     s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
-  HIP_TRY(hipGetLastError());
-  return kOk;
-}
-
 template <int BITS>
 int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf_block* vcw,
                        int E, int party, int store_bytes, hipStream_t s) {
-  int t = 0, D = 0;
-  const int64_t starts = p.num_items >> p.k0;
-  if (small_shape(starts, p.num_levels, &t, &D))
-    return d->kind[0] == DPF_LEAF_XOR
-               ? launch_small<BITS, true>(p, starts, t, D, vcw, E, party, store_bytes, s)
-               : launch_small<BITS, false>(p, starts, t, D, vcw, E, party, store_bytes, s);
+  if (d->kind[0] == DPF_LEAF_XOR ? try_small(p, FastIntLeaf<BITS, true>{vcw, E, party, store_bytes, {}}, s)
+                                 : try_small(p, FastIntLeaf<BITS, false>{vcw, E, party, store_bytes, {}}, s)) {
+    HIP_TRY(hipGetLastError());
+    return kOk;
+  }
   if (d->kind[0] == DPF_LEAF_XOR ? launch_octet<BITS, true>(p, vcw, E, party, store_bytes, s)
                                  : launch_octet<BITS, false>(p, vcw, E, party, store_bytes, s)) {
     HIP_TRY(hipGetLastError());
@@ -1389,15 +1400,14 @@ void prefault(char* p, size_t bytes, int threads) {
   for (auto& th : pool) th.join();
 }
 
-// A fresh destination of kRegisterMin..kPipelineMax is mapped and registered
-// piece by piece behind the DMA; a larger one whole before the first DMA (the
-// r13 path).  DPF_HIP_D2H_PIPELINE=0 / =1 (read per call) forces either: A/B
-// and test hooks.
-constexpr size_t kPipelineMax = size_t{16} << 30;   // see piece_bytes below
-bool d2h_pipeline_on(size_t bytes) {
+// A fresh destination of >= kRegisterMin is mapped and registered piece by
+// piece behind the DMA (see piece_bytes below for the piece sizes).
+// DPF_HIP_D2H_PIPELINE=0 (read per call) maps and registers the whole range
+// before the first DMA instead (the r13 path): the A/B and test hook.
+constexpr size_t kPipelineMax = size_t{16} << 30;   // above: a few large pieces
+bool d2h_pipeline_on(size_t) {
   const char* v = std::getenv("DPF_HIP_D2H_PIPELINE");
-  if (v && v[0] == '1') return true;   // force (probes)
-  return !(v && v[0] == '0') && bytes <= kPipelineMax;
+  return !(v && v[0] == '0');
 }
 // DPF_HIP_D2H_REGISTER_PIECES=<n> (read per call): the pipelined copy acts as
 // if the registration of its piece n (and every later one) were refused -- a
@@ -1417,14 +1427,13 @@ long register_pieces_limit() {
 // the bounce buffers.
 constexpr size_t kPiece = size_t{256} << 20;
 constexpr int kNoHelperThread = -1000;   // pipelined_d2h could not start its helper
-// At most ~32 pieces (256 MiB up to 8 GiB), and only up to kPipelineMax: a
-// 32 GiB copy (config 3's 2^31 uint128) ran 1.0-1.45 s pipelined, but in 1 of
-// 4 calls its DMA alone took ~2.65 s (13 GB/s; the helper thread never
-// behind, the value-initialisation on the calling thread 1.0-1.4 s either
-// way), with 129 pieces or 33; mapped and registered whole first it ran
-// 1.27-1.62 s in every call (profiles/r14_u128_reps_probe.txt).  8 GiB copies
-// never showed the slow mode (164-171 ms pipelined vs 199-209 ms).  A/B hooks
-// (read per call): DPF_HIP_D2H_PIECE_MIB (a multiple of 64) and
+// Up to kPipelineMax: ~32 pieces (256 MiB up to 8 GiB; 8 GiB copies 164-171
+// ms pipelined vs 199-209 ms registered whole).  Above it, 8 GiB pieces: a
+// 32 GiB copy (config 3's 2^31 uint128) in 33 or 129 pieces ran its DMA at
+// ~13 GB/s in 1 of 4 calls (r14) and 3 of 6 (r15), in 5 pieces never in 6
+// calls (3 pieces: never in 6), 682-758 ms per copy against 801-938 ms
+// registered whole first (profiles/r15_ab.txt part 12).  A/B hooks (read per
+// call): DPF_HIP_D2H_PIECE_MIB (a multiple of 64) and
 // DPF_HIP_D2H_PREFAULT_THREADS (default 8).
 
 size_t piece_bytes(size_t bytes) {
@@ -1432,6 +1441,7 @@ size_t piece_bytes(size_t bytes) {
   const long m = v && *v ? std::strtol(v, nullptr, 10) : 0;
   if (m >= 64 && m % 64 == 0) return static_cast<size_t>(m) << 20;
   const size_t step = size_t{64} << 20;
+  if (bytes > kPipelineMax) return size_t{8} << 30;
   const size_t want = (bytes / 32 + step - 1) / step * step;
   return want > kPiece ? want : kPiece;
 }
@@ -1960,6 +1970,10 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
         off += b;
       }
       const char* off_env = getenv("DPF_EXPAND_NO_OCTET");
+      if (try_small(p, w, s)) {
+        HIP_TRY(hipGetLastError());
+        return kOk;
+      }
       if (p.S >= 3 && !(off_env && off_env[0] == '1')) {
         note_expand<SwarLeaf>(p, true);
         const int blk = block_for(p.num_items);
@@ -1986,6 +2000,10 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       Mod32Leaf<2> m;
       fill(m);
       const char* off = getenv("DPF_EXPAND_NO_OCTET");
+      if (try_small(p, m, s)) {
+        HIP_TRY(hipGetLastError());
+        return kOk;
+      }
       if (p.S >= 3 && !(off && off[0] == '1')) {
         // Octet form (the half's four leaves hashed as two ILP4 groups).
         note_expand<Mod32Leaf<2>>(p, true);

@@ -237,6 +237,26 @@ def test_expand_small_trees(hip, vt, levels, n0, cepb, party, monkeypatch):
     assert not hip.last_expand_kernel()[0].startswith("small/")
 
 
+# The small-tree launch takes the other leaf policies too (Leaf::emit2 for
+# the last level): SwarLeaf, Mod32Leaf<2>, Mod32Leaf<4>.  GenericLeaf is not
+# dispatched to it (spills there; measured no faster): "pair/generic".
+@pytest.mark.parametrize("vt,want", [
+    (("tuple", [("int", 8), ("xor", 8)]), "small/swar"),
+    (("tuple", [("intmodn", 32, M32), ("intmodn", 32, M32)]), "small/mod32"),
+    (("tuple", [("intmodn", 32, M32)] * 4), "small/mod32"),
+    (("tuple", [("int", 32), ("int", 128)]), "pair/generic"),
+    (("tuple", [("intmodn", 64, M64)] * 5), "pair/generic")], ids=str)
+@pytest.mark.parametrize("levels,n0", [(12, 1), (9, 3)])
+@pytest.mark.parametrize("party", [0, 1])
+def test_expand_small_trees_all_leaves(hip, vt, want, levels, n0, party, monkeypatch):
+    seed = hash((str(vt), levels, n0, party, "small-leaves")) & 0xFFFFFFFF
+    _expand_case(hip, np.random.default_rng(seed), vt, n0, levels, party, sec=40.0)
+    assert hip.last_expand_kernel()[0] == want
+    monkeypatch.setenv("DPF_EXPAND_SMALL", "0")
+    _expand_case(hip, np.random.default_rng(seed), vt, n0, levels, party, sec=40.0)
+    assert not hip.last_expand_kernel()[0].startswith("small/")
+
+
 # Start counts that are not powers of two: dpf_hip_expand picks the subtree
 # depth by the per-thread critical path (5 starts x 2^21: depth 4, 5 * 2^17
 # subtrees in 3 even rounds, where "fill the launch" gave depth 5 in 2 rounds).

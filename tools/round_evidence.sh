@@ -11,8 +11,9 @@
 #          drop-in API (default allocator and --malloc_keep_pages);
 #   part2: profile + bench line of config 3 (uint128) and the two tuple kernels;
 #   part3: profile + bench line of config 4 (EvaluateAt per key and summed) and DCF;
-#   part4: profile + bench line of config 5b (heavy hitters), then the
-#          synthetic-benchmark lines (no kernel profile of their own).
+#   part4: profile + bench line of config 5b (heavy hitters), then config 1's
+#          line (log 20, latency mode) and the synthetic-benchmark lines (no
+#          kernel profile of their own).
 # Each profile is tools/profile_workload.sh: a kernel trace and four PMC
 # passes of the SAME bench command, summarised per workload into
 # gpurun_out/<tag>_<workload>_summary.json (copied to profiles/ afterwards).
@@ -48,7 +49,7 @@ part1)
   timeout -k 10 300 python bench.py > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err || { tail -20 $O/${TAG}_bench.err; exit 1; }
   cat $O/${TAG}_bench.json
   timeout -k 10 300 python bench.py --host-output --no-cpu-baseline --steps 5 --warmup 1 > $O/${TAG}_api_u64.json 2> $O/${TAG}_api_u64.err || { tail -20 $O/${TAG}_api_u64.err; exit 1; }
-  timeout -k 10 400 python bench.py --workload full_domain_u128 --host-output --no-cpu-baseline --steps 3 --warmup 1 > $O/${TAG}_api_u128.json 2> $O/${TAG}_api_u128.err || { tail -20 $O/${TAG}_api_u128.err; exit 1; }
+  timeout -k 10 500 python bench.py --workload full_domain_u128 --host-output --host-output-reps 6 --no-cpu-baseline --steps 3 --warmup 1 > $O/${TAG}_api_u128.json 2> $O/${TAG}_api_u128.err || { tail -20 $O/${TAG}_api_u128.err; exit 1; }
   echo "api lines ok"
   timeout -k 10 600 distributed_point_functions_amd/lib/dpf_benchmark > $O/${TAG}_reference_benchmarks.txt 2> $O/${TAG}_reference_benchmarks.err || { tail -5 $O/${TAG}_reference_benchmarks.err; exit 1; }
   timeout -k 10 300 distributed_point_functions_amd/lib/dpf_benchmark --malloc_keep_pages "--benchmark_filter=^BM_EvaluateRegularDpf" > $O/${TAG}_reference_benchmarks_keep_pages.txt 2>&1 || exit 1
@@ -65,6 +66,7 @@ part3)
   ;;
 part4)
   PROFILE_PASS_LIMIT=400 profline heavy_hitters "hh_level_kernel|batch_level_kernel<Mod32V<2, true>, 2, true>|gather_seeds_kernel|finalize_sums_kernel" total:2 heavy_hitters "--no-cpu-baseline" --workload heavy_hitters
+  line config1 --log-domain 20 --steps 500 --warmup 50
   line syn_dev32 --workload synthetic_hierarchical_device --domain 32
   line syn_dev128 --workload synthetic_hierarchical_device --domain 128
   line syn_h32 --workload synthetic_hierarchical --domain 32
