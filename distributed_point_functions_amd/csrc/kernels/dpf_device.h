@@ -538,8 +538,10 @@ inline Div32 make_div32(uint32_t n) {
 
 
 
-// Tuples of IntModN<uint32_t, N < 2^32> sampled from <= 2 blocks.
-constexpr int kMod32MaxLeaves = 4;
+// Tuples of IntModN<uint32_t, N < 2^32> sampled from <= 2 blocks: 16 + 4 (nl - 1)
+// bytes <= 32, so at most five leaves (the reference benchmark's
+// Tuple<IntModN<uint32_t, 2^32 - 5> x5> among them).
+constexpr int kMod32MaxLeaves = 5;
 inline bool mod32_eligible(const dpf_value_desc* d, int* blocks_read) {
   if (d->direct || d->elements_per_block != 1 || d->num_leaves > kMod32MaxLeaves) return false;
   for (int k = 0; k < d->num_leaves; ++k)
@@ -674,7 +676,9 @@ struct Mod32Leaf {
         }
         if (party == 1) r = r == 0 ? 0u : n - r;
         x[i] = r;
-        blk[0] = w[4 + i]; blk[1] = q[0]; blk[2] = q[1]; blk[3] = q[2];
+        if (i + 1 < NLMAX) {   // the next leaf's block (w[4 + i]: at most w[7])
+          blk[0] = w[4 + i]; blk[1] = q[0]; blk[2] = q[1]; blk[3] = q[2];
+        }
       } else {
         x[i] = 0;
       }

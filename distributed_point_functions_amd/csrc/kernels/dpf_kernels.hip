@@ -761,7 +761,7 @@ template <class Leaf>
 const char* leaf_name() {
   if constexpr (std::is_same_v<Leaf, SwarLeaf>) return "swar";
   else if constexpr (std::is_same_v<Leaf, GenericLeaf>) return "generic";
-  else if constexpr (std::is_same_v<Leaf, Mod32Leaf<2>> ||
+  else if constexpr (std::is_same_v<Leaf, Mod32Leaf<2>> || std::is_same_v<Leaf, Mod32Leaf<4>> ||
                      std::is_same_v<Leaf, Mod32Leaf<kMod32MaxLeaves>>) return "mod32";
   else return "fast";
 }
@@ -2013,6 +2013,11 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
         HIP_TRY(hipGetLastError());
         return kOk;
       }
+      return launch_expand(p, m, s);
+    }
+    if (desc->num_leaves <= 4) {   // no spills (Mod32Leaf<5> in expand_kernel: 36 B)
+      Mod32Leaf<4> m;
+      fill(m);
       return launch_expand(p, m, s);
     }
     Mod32Leaf<kMod32MaxLeaves> m;

@@ -175,6 +175,8 @@ SPECIALISED_TYPES = [
     ("tuple", [("intmodn", 32, 2147483647)] * 2),
     ("intmodn", 32, 3),
     ("tuple", [("intmodn", 32, 2147483648)] * 2),
+    # Five IntModN32 leaves: the most that two hashed blocks can sample.
+    ("tuple", [("intmodn", 32, M32)] * 5),
 ]
 
 
@@ -191,10 +193,11 @@ def test_expand_specialised_leaves(hip, vt, party, sec):
 # SwarLeaf, Mod32Leaf<2>); both that launch and the pair kernel
 # (DPF_EXPAND_NO_OCTET=1) must match the oracle, and the dispatch is checked.
 # Expected launch per type: Tuple<uint16_t x3> stores 12-byte leaves and 3 or
-# 4 IntModN32 leaves use Mod32Leaf<4>, both on the pair kernel.
+# 4 (or 5) IntModN32 leaves use Mod32Leaf<5>, both on the pair kernel.
 EXPECTED_KERNEL = ["octet/fast", "pair/fast", "octet/swar", "octet/swar", "octet/swar",
                    "octet/swar", "octet/swar", "octet/mod32", "octet/mod32", "pair/mod32",
-                   "octet/mod32", "pair/mod32", "octet/mod32", "octet/mod32", "octet/mod32"]
+                   "octet/mod32", "pair/mod32", "octet/mod32", "octet/mod32", "octet/mod32",
+                   "pair/mod32"]
 
 
 @pytest.mark.parametrize("i", range(len(SPECIALISED_TYPES)),
@@ -238,12 +241,13 @@ def test_expand_small_trees(hip, vt, levels, n0, cepb, party, monkeypatch):
 
 
 # The small-tree launch takes the other leaf policies too (Leaf::emit2 for
-# the last level): SwarLeaf, Mod32Leaf<2>, Mod32Leaf<4>.  GenericLeaf is not
+# the last level): SwarLeaf, Mod32Leaf<2>, Mod32Leaf<5>.  GenericLeaf is not
 # dispatched to it (spills there; measured no faster): "pair/generic".
 @pytest.mark.parametrize("vt,want", [
     (("tuple", [("int", 8), ("xor", 8)]), "small/swar"),
     (("tuple", [("intmodn", 32, M32), ("intmodn", 32, M32)]), "small/mod32"),
     (("tuple", [("intmodn", 32, M32)] * 4), "small/mod32"),
+    (("tuple", [("intmodn", 32, M32)] * 5), "small/mod32"),
     (("tuple", [("int", 32), ("int", 128)]), "pair/generic"),
     (("tuple", [("intmodn", 64, M64)] * 5), "pair/generic")], ids=str)
 @pytest.mark.parametrize("levels,n0", [(12, 1), (9, 3)])
