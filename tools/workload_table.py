@@ -15,6 +15,8 @@ ROWS = [
     # (bench file suffix, label, result formatter)
     ("full_domain", "config 2 full domain (2^30 uint64)",
      lambda d: f"{d['value'] / 1e9:.1f} G leaves/s, {d['ms_per_step']:.2f} ms per step"),
+    ("config1", "config 1 full domain (2^20 uint64, latency mode)",
+     lambda d: f"{d['value'] / 1e9:.1f} G leaves/s, {d['ms_per_step'] * 1e3:.1f} us per step"),
     ("full_domain_u128", "config 3 shard (2^31 uint128 per GPU)",
      lambda d: f"{d['value'] / 1e9:.1f} G leaves/s, {d['ms_per_step']:.1f} ms"),
     ("tuple_u32", "Tuple<uint32_t, uint32_t> full domain (2^30)",
@@ -45,7 +47,7 @@ def cpu(d):
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r14"
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r15"
     print("| workload | result | G AES/s | VALU roofline | clock (GHz, profile) | CPU baseline (16 host threads) |")
     print("|---|---|---|---|---|---|")
     for suffix, label, fmt in ROWS:
