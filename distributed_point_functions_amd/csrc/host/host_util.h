@@ -358,7 +358,12 @@ class HostStaging {
 // device addresses, valid until the next Reset().  Reset() waits for the
 // previous call's stream, so neither the page-locked image nor the device
 // arena is rewritten while a copy or kernel still reads it.  Images above
-// kMaxPinned are built in pageable memory and copied synchronously.
+// kMaxPinned are built in pageable memory and copied synchronously.  Images
+// of at most kZeroCopyMax (128 KiB) bytes are not copied at all: the kernels read them
+// from the page-locked image itself (ROCm maps page-locked host memory into
+// the device's address space), which saves a small call the ~5 us latency of
+// one DMA (profiles/r13_latency_microbench.txt); DPF_UPLOAD_ZERO_COPY=0
+// (read per call) copies them too (A/B and test hook).
 class PackedUploads {
  public:
   PackedUploads() = default;
@@ -372,8 +377,16 @@ class PackedUploads {
   // Waits for the previous call's copy and kernel (an event recorded on its
   // stream after the launch, MarkUsed) before the buffers are rewritten.
   Status Reset() {
-    if (pending_) HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
+    if (pending_) {
+      HIP_RETURN_IF_ERROR(dpf_hip_event_sync(event_));
+    } else if (unmarked_) {
+      // A zero-copy image whose caller returned before MarkUsed (an error
+      // after Commit): whatever it launched may still read the image.
+      HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(commit_stream_));
+    }
     pending_ = false;
+    unmarked_ = false;
+    zero_copy_ = false;
     size_ = 0;
     pageable_ = false;
     return OkStatus();
@@ -386,6 +399,7 @@ class PackedUploads {
     if (!event_) HIP_RETURN_IF_ERROR(dpf_hip_event_create(&event_));
     HIP_RETURN_IF_ERROR(dpf_hip_event_record(event_, stream));
     pending_ = true;
+    unmarked_ = false;
     return OkStatus();
   }
   // Space for `count` elements of T in the image, to be filled by the caller
@@ -411,17 +425,29 @@ class PackedUploads {
       DPF_RETURN_IF_ERROR(arena_.Reserve(size_));
       return FromHip(dpf_hip_memcpy_h2d(arena_.get(), image_.get(), size_, stream));
     }
+    if (size_ <= kZeroCopyMax && ZeroCopyOn()) {
+      zero_copy_ = true;
+      unmarked_ = true;
+      commit_stream_ = stream;
+      return OkStatus();
+    }
     DPF_RETURN_IF_ERROR(arena_.Reserve(cap_));
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(arena_.get(), pinned_, size_, stream));
     return MarkUsed(stream);
   }
   template <typename T>
   T* Ptr(size_t off) const {
-    return reinterpret_cast<T*>(static_cast<char*>(arena_.get()) + off);
+    return reinterpret_cast<T*>((zero_copy_ ? static_cast<char*>(pinned_)
+                                            : static_cast<char*>(arena_.get())) + off);
   }
 
  private:
   static constexpr size_t kMaxPinned = size_t{64} << 20;
+  static constexpr size_t kZeroCopyMax = size_t{128} << 10;
+  static bool ZeroCopyOn() {
+    const char* v = std::getenv("DPF_UPLOAD_ZERO_COPY");
+    return !(v && v[0] == '0');
+  }
   char* base() { return pageable_ ? image_.get() : static_cast<char*>(pinned_); }
   // Pageable image of at least `end` bytes holding [0, size_) of the current one
   // (uninitialised beyond: no value-initialisation pass over a large image).
@@ -463,6 +489,9 @@ class PackedUploads {
   size_t cap_ = 0;
   DeviceBuffer arena_;
   bool pending_ = false;
+  bool zero_copy_ = false;   // this call's kernels read pinned_ itself
+  bool unmarked_ = false;    // zero-copy Commit not yet followed by MarkUsed
+  void* commit_stream_ = nullptr;
   void* event_ = nullptr;
 };
 
