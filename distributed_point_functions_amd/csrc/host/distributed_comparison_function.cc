@@ -230,16 +230,24 @@ StatusOr<std::vector<uint8_t>> DistributedComparisonFunction::EvaluatePacked(
   const size_t o_vcw = up.Add(vcw_all.data(), vcw_all.size());
   const size_t o_pts = up.Add(pts.data(), pts.size());
   DPF_RETURN_IF_ERROR(up.Commit(nullptr));
-  DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(m) * f.packed_size));
+  const size_t bytes = static_cast<size_t>(m) * f.packed_size;
+  void* small = s->small_out.Get(bytes);   // small results: written to page-locked memory
+  if (!small) DPF_RETURN_IF_ERROR(s->out.Reserve(bytes));
+  void* const dev_out = small ? small : s->out.get();
   std::vector<const dpf_block*> vcw(n);
   for (int i = 0; i < n; ++i) vcw[i] = up.Ptr<dpf_block>(o_vcw) + vcw_off[i];
   DPF_RETURN_IF_ERROR(Launch(1, m, false, up.Ptr<dpf_block>(o_seed), up.Ptr<uint8_t>(o_party),
                              up.Ptr<dpf_block>(o_pts), up.Ptr<dpf_block>(o_cws),
                              up.Ptr<uint8_t>(o_cwl), up.Ptr<uint8_t>(o_cwr), L, vcw,
-                             s->out.get(), nullptr));
+                             dev_out, nullptr));
   DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
-  std::vector<uint8_t> out(m * f.packed_size);
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
+  std::vector<uint8_t> out(bytes);
+  if (small) {
+    HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(nullptr));
+    std::memcpy(out.data(), small, bytes);
+  } else {
+    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(out.data(), s->out.get(), out.size(), nullptr));
+  }
   return out;
 }
 

@@ -668,10 +668,16 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     for (int64_t i = 0; identity && i < num_prefixes; ++i)
       identity = prefix_map[i].first == i && prefix_map[i].second == 0;
   }
+  // A small host result is written by the kernels straight into page-locked
+  // memory (PinnedOut): no D2H copy.
+  void* small = (!device_out && host_out) ? s->small_out.Get(static_cast<size_t>(total) * esz)
+                                          : nullptr;
   void* expand_out = nullptr;
   if (device_out && identity) {
     if (capacity_bytes < total * esz) return InvalidArgumentError("device output buffer too small");
     expand_out = device_out;
+  } else if (small && identity) {
+    expand_out = small;
   } else {
     DPF_RETURN_IF_ERROR(s->out.Reserve(static_cast<size_t>(corrected) * esz));
     expand_out = s->out.get();
@@ -716,6 +722,8 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
     if (device_out) {
       if (capacity_bytes < total * esz) return InvalidArgumentError("device output buffer too small");
       result = device_out;
+    } else if (small) {
+      result = small;
     } else {
       DPF_RETURN_IF_ERROR(s->gathered.Reserve(static_cast<size_t>(total) * esz));
       result = s->gathered.get();
@@ -726,6 +734,12 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   clk.mark(2);
   if (!device_out) {
     const size_t bytes = static_cast<size_t>(total) * esz;
+    if (small) {
+      clk.mark(3);
+      DPF_RETURN_IF_ERROR(dpf_internal::ConsumePinnedOut(*host_out, small, bytes, stream));
+      clk.mark(4);
+      return OkStatus();
+    }
     void* dst = host_out->reserve(bytes);
     clk.mark(3);
     HIP_RETURN_IF_ERROR(CopyToHostSink(*host_out, dst, result, bytes, stream, &parts));
@@ -974,7 +988,9 @@ Status DistributedPointFunction::EvaluateAtToHost(const DpfKey& key, int hierarc
   clk.mark(1);
   DPF_RETURN_IF_ERROR(up.Commit(nullptr));
   const size_t bytes = static_cast<size_t>(n) * f.packed_size;
-  DPF_RETURN_IF_ERROR(s->out.Reserve(bytes));
+  void* small = s->small_out.Get(bytes);   // small results: written to page-locked memory
+  if (!small) DPF_RETURN_IF_ERROR(s->out.Reserve(bytes));
+  void* const out = small ? small : s->out.get();
   clk.mark(2);
   const dpf_value_desc desc = MakeDesc(f, blocks_needed_[hierarchy_level]);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
@@ -982,8 +998,7 @@ Status DistributedPointFunction::EvaluateAtToHost(const DpfKey& key, int hierarc
       n, n, L, up.Ptr<dpf_block>(o_root), up.Ptr<uint8_t>(o_party),
       ctx ? start.seeds : nullptr, ctx ? start.ctrl : nullptr, up.Ptr<dpf_block>(o_paths),
       up.Ptr<int32_t>(o_bi), up.Ptr<dpf_block>(o_cw.seed), up.Ptr<uint8_t>(o_cw.left),
-      up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), s->out.get(),
-      nullptr));
+      up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), out, nullptr));
   DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
   clk.mark(3);
   if (g_until_timing_on) {
@@ -993,8 +1008,12 @@ Status DistributedPointFunction::EvaluateAtToHost(const DpfKey& key, int hierarc
   // Packed elements straight into the caller's result (h:983-1003 outputs):
   // integers copied, tuples / IntModN / XorWrapper unpacked chunk by chunk out
   // of the page-locked staging buffers.
-  HIP_RETURN_IF_ERROR(dpf_internal::CopyToHostSink(sink, sink.reserve(bytes), s->out.get(), bytes,
-                                                   nullptr));
+  if (small) {
+    DPF_RETURN_IF_ERROR(dpf_internal::ConsumePinnedOut(sink, small, bytes, nullptr));
+  } else {
+    HIP_RETURN_IF_ERROR(dpf_internal::CopyToHostSink(sink, sink.reserve(bytes), s->out.get(), bytes,
+                                                     nullptr));
+  }
   clk.mark(5);
   if (ctx) ctx->set_previous_hierarchy_level(hierarchy_level);
   return OkStatus();

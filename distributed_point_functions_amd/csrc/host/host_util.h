@@ -535,6 +535,45 @@ class StreamFence {
   void* last_stream_ = nullptr;
 };
 
+// Page-locked memory for the result of a small call (<= 1 MiB): the kernel
+// writes it over PCIe and the host reads it after a stream sync -- no D2H
+// DMA and its ~5 us of latency (profiles/r13_latency_microbench.txt).
+// DPF_OUTPUT_ZERO_COPY=0 (read per call) turns it off (A/B and test hook).
+class PinnedOut {
+ public:
+  PinnedOut() = default;
+  PinnedOut(const PinnedOut&) = delete;
+  PinnedOut& operator=(const PinnedOut&) = delete;
+  ~PinnedOut() {
+    if (p_) dpf_hip_host_free(p_);
+  }
+  // Page-locked room for `bytes`, or nullptr (too large, off, or no memory).
+  void* Get(size_t bytes) {
+    const char* v = std::getenv("DPF_OUTPUT_ZERO_COPY");
+    if (bytes == 0 || bytes > kMax || (v && v[0] == '0')) return nullptr;
+    if (!p_ && dpf_hip_host_alloc(&p_, kMax) != 0) p_ = nullptr;
+    return p_;
+  }
+
+ private:
+  static constexpr size_t kMax = size_t{1} << 20;
+  void* p_ = nullptr;
+};
+
+// Hands `bytes` of a result the kernels wrote to page-locked memory `p` (on
+// `stream`) to a HostSink.
+inline Status ConsumePinnedOut(const HostSink& sink, const void* p, size_t bytes, void* stream) {
+  HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+  void* dst = sink.reserve(bytes);
+  if (sink.chunk) {
+    sink.chunk(static_cast<const uint8_t*>(p), 0, bytes);
+    return OkStatus();
+  }
+  if (sink.grow) sink.grow(bytes);
+  std::memcpy(dst, p, bytes);
+  return OkStatus();
+}
+
 // The device buffers and staging of one DistributedPointFunction (or
 // DistributedComparisonFunction).  The reference's const evaluation methods
 // may be called from several threads at once; `mu` makes every call that
@@ -548,6 +587,7 @@ class DeviceScratch {
   DeviceBuffer key_seed, party, block_index, workspace;
   StreamFence workspace_fence;  // the sum kernels' 192-bit accumulators
   HostStaging staging;
+  PinnedOut small_out;           // results of small calls, written by the kernels
   template <typename T>
   Status Upload(DeviceBuffer& dst, const T* data, size_t count, void* stream = nullptr) {
     return staging.Upload(dst, data, count * sizeof(T), stream);
