@@ -561,16 +561,21 @@ class PinnedOut {
 };
 
 // Hands `bytes` of a result the kernels wrote to page-locked memory `p` (on
-// `stream`) to a HostSink.
+// `stream`) to a HostSink; a sink that throws (no memory for the result)
+// is reported as an internal error, as the chunked D2H path does.
 inline Status ConsumePinnedOut(const HostSink& sink, const void* p, size_t bytes, void* stream) {
   HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
-  void* dst = sink.reserve(bytes);
-  if (sink.chunk) {
-    sink.chunk(static_cast<const uint8_t*>(p), 0, bytes);
-    return OkStatus();
+  try {
+    void* dst = sink.reserve(bytes);
+    if (sink.chunk) {
+      sink.chunk(static_cast<const uint8_t*>(p), 0, bytes);
+      return OkStatus();
+    }
+    if (sink.grow) sink.grow(bytes);
+    std::memcpy(dst, p, bytes);
+  } catch (const std::exception& e) {
+    return InternalError(std::string("copying a small result to host memory failed: ") + e.what());
   }
-  if (sink.grow) sink.grow(bytes);
-  std::memcpy(dst, p, bytes);
   return OkStatus();
 }
 
