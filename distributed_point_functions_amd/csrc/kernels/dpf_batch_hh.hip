@@ -35,6 +35,14 @@ using namespace dpf_rt;
 
 // 1: the second leaf pair waits in LDS (32 B per thread beside the 128 KiB of
 // tables) while the first pair is hashed, instead of in 10 VGPRs.
+// DPF_HH_PREFETCH=1: the next key's start seed is loaded before this key's
+// value hashes (the start seeds come from scattered rows of the expansion
+// cache since the slot-table rewrite).  Measured slower (128 VGPRs; 2^20
+// clients 20.68 vs 20.52 s per pass, 2^18 5.41 vs 5.33 s, profiles/r15_ab.txt
+// part 17): the other 15 waves of the CU already hide the load.  Off.
+#ifndef DPF_HH_PREFETCH
+#define DPF_HH_PREFETCH 0
+#endif
 #ifndef DPF_HH_STASH
 #define DPF_HH_STASH 1
 #endif
@@ -154,11 +162,25 @@ void hh_level_kernel(HHParams p) {
     uint32_t acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = 0;
+#if DPF_HH_PREFETCH
+    Block4 s_next{};
+    uint32_t c_next = 0;
+    if (k_begin < k_end) {
+      s_next = load_block(p.seeds_in + k_begin * p.in_stride + par);
+      if (p.ctrl_in) c_next = p.ctrl_in[k_begin * p.in_stride + par];
+    }
+#endif
     for (int64_t k = k_begin; k < k_end; ++k) {
+#if DPF_HH_PREFETCH
+      Block4 s = s_next;
+      const uint32_t c_in = c_next;
+#else
       Block4 s = load_block(p.seeds_in + k * p.in_stride + par);
+      const uint32_t c_in = p.ctrl_in ? p.ctrl_in[k * p.in_stride + par] : 0u;
+#endif
       uint32_t t;
       if (p.ctrl_in) {
-        t = p.ctrl_in[k * p.in_stride + par] & 1u;
+        t = c_in & 1u;
       } else {
         t = s.w0 & 1u;
         s.w0 &= ~1u;
@@ -205,6 +227,15 @@ void hh_level_kernel(HHParams p) {
       const uint32_t corr[2] = {(uint32_t)vc[0].low, p.nl > 1 ? (uint32_t)vc[1].low : 0u};
       const UniformRK rk[4] = {UniformRK{lk.ks.v}, UniformRK{lk.ks.v}, UniformRK{lk.ks.v},
                                UniformRK{lk.ks.v}};
+#if DPF_HH_PREFETCH
+      {
+        // In-place rewrites are safe: the next key's row is not written until
+        // that key's own iteration (leaf stores go to row k only).
+        const int64_t kn = k + 1 < k_end ? k + 1 : k;
+        s_next = load_block(p.seeds_in + kn * p.in_stride + par);
+        if (p.ctrl_in) c_next = p.ctrl_in[kn * p.in_stride + par];
+      }
+#endif
 #if DPF_HH_STASH
       lds.stash[0][threadIdx.x] = make_uint4(L[2].w0 | tl[2], L[2].w1, L[2].w2, L[2].w3);
       lds.stash[1][threadIdx.x] = make_uint4(L[3].w0 | tl[3], L[3].w1, L[3].w2, L[3].w3);
