@@ -93,18 +93,51 @@ struct HHParams {
 
 // value = sampled IntModN elements of one leaf (value_type_helpers.h:286-311):
 // r0 = block mod N0; r1 = ((block / N0) << 32 | next 4 bytes) mod N1.
-__device__ __forceinline__ void sample2(const HHParams& p, const Block4& h0, uint32_t w4,
-                                        uint32_t out[2]) {
+__device__ __forceinline__ void sample2(const HHParams& p, const Div32 (&div)[2], const Block4& h0,
+                                        uint32_t w4, uint32_t out[2]) {
   const uint32_t blk[4] = {h0.w0, h0.w1, h0.w2, h0.w3};
   uint32_t q[3];
-  out[0] = divmod128(blk, p.div[0], q);
+  out[0] = divmod128(blk, div[0], q);
   if (p.nl > 1) {
     const uint32_t nb[4] = {w4, q[0], q[1], q[2]};
     uint32_t q2[3];
-    out[1] = divmod128(nb, p.div[1], q2);
+    out[1] = divmod128(nb, div[1], q2);
   } else {
     out[1] = 0;
   }
+}
+
+// DPF_HH_PIN_DIV=1: wave-uniform kernel arguments copied into SGPRs by an
+// instruction the compiler cannot rematerialise, so under SGPR pressure it
+// spills the copy to a VGPR lane (v_writelane / v_readlane, no wait) instead
+// of reloading the argument with s_load, whose lgkmcnt(0) wait drains the
+// LDS lookups in flight (party / leaf_seeds / leaf_stride were reloaded 10x
+// per key, r15 ISA).  Measured slower (2^20 clients 20.57 vs 20.45 s per
+// pass, 2^18 5.39 / 5.37 vs 5.32 / 5.33 s; profiles/r15_ab.txt part 18): off.
+#ifndef DPF_HH_PIN_DIV
+#define DPF_HH_PIN_DIV 0
+#endif
+__device__ __forceinline__ uint32_t pin_sgpr(uint32_t x) {
+#if DPF_HH_PIN_DIV
+  uint32_t r;
+  asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(x));
+  return r;
+#else
+  return x;
+#endif
+}
+__device__ __forceinline__ uint64_t pin_sgpr64(uint64_t x) {
+#if DPF_HH_PIN_DIV
+  uint64_t r;
+  asm volatile("s_mov_b64 %0, %1" : "=s"(r) : "s"(x));
+  return r;
+#else
+  return x;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ T* pin_ptr(T* x) {
+  return reinterpret_cast<T*>(pin_sgpr64(reinterpret_cast<uint64_t>(x)));
 }
 
 __device__ __forceinline__ uint32_t mod_add(uint32_t a, uint32_t b, uint32_t n) {
@@ -148,6 +181,16 @@ void hh_level_kernel(HHParams p) {
                      {lt, lt + 128u, lt + 65536u, lt + 65664u}, m1,
                      KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), KeyRef{}}};
   const int64_t U = p.num_starts;
+  // The arguments the key loop reads every key (the s_load_dwordx8 of
+  // party / wide / leaf_seeds / leaf_stride was reloaded 10x per key).
+  const uint8_t* const party_p = pin_ptr(p.party);
+  dpf_block* const leaf_seeds = pin_ptr(p.leaf_seeds);
+  const int64_t leaf_stride = (int64_t)pin_sgpr64((uint64_t)p.leaf_stride);
+  Div32 div[2];
+#pragma unroll
+  for (int e = 0; e < 2; ++e)
+    div[e] = Div32{pin_sgpr(p.div[e].dn), pin_sgpr(p.div[e].v), (int)pin_sgpr((uint32_t)p.div[e].sh),
+                   pin_sgpr(p.div[e].n)};
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.num_threads;
        g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t wave = g >> 6;
@@ -162,6 +205,12 @@ void hh_level_kernel(HHParams p) {
     uint32_t acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = 0;
+    // The node's four leaf slots (the same for every key), loaded once: inside
+    // the key loop the compiler reloaded them every key (the leaf stores may
+    // alias the table), one more wait per key.
+    int4 sl = make_int4((int)(u << 2), (int)(u << 2) + 1, (int)(u << 2) + 2, (int)(u << 2) + 3);
+    if (p.leaf_slot && leaf_seeds && valid)
+      sl = *reinterpret_cast<const int4*>(p.leaf_slot + (u << 2));
 #if DPF_HH_PREFETCH
     Block4 s_next{};
     uint32_t c_next = 0;
@@ -206,13 +255,11 @@ void hh_level_kernel(HHParams p) {
       Block4 L[4];
       uint32_t tl[4];
       children_step_x2(lk, lk.ks.l, lk.ks.r, c0, t0, c1, t1, cs1, cc1, L, tl);
-      if (p.leaf_seeds && valid) {
+      if (leaf_seeds && valid) {
         // A slot table places the leaves when the cache is rewritten in place:
         // leaf 0 in this node's own slot (read above by this thread), the
         // others in slots no start node reads.
-        dpf_block* o = p.leaf_seeds + k * p.leaf_stride;
-        int4 sl = make_int4((int)(u << 2), (int)(u << 2) + 1, (int)(u << 2) + 2, (int)(u << 2) + 3);
-        if (p.leaf_slot) sl = *reinterpret_cast<const int4*>(p.leaf_slot + (u << 2));
+        dpf_block* o = leaf_seeds + k * leaf_stride;
         const int slot[4] = {sl.x, sl.y, sl.z, sl.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -222,7 +269,7 @@ void hh_level_kernel(HHParams p) {
         }
       }
       // Value hashes (cc:500-524): two leaves' b blocks per ILP4 group.
-      const int party = p.party[k] & 1;
+      const int party = party_p[k] & 1;
       const dpf_block* vc = p.vcw + k * p.vcw_stride;
       const uint32_t corr[2] = {(uint32_t)vc[0].low, p.nl > 1 ? (uint32_t)vc[1].low : 0u};
       const UniformRK rk[4] = {UniformRK{lk.ks.v}, UniformRK{lk.ks.v}, UniformRK{lk.ks.v},
@@ -268,11 +315,11 @@ void hh_level_kernel(HHParams p) {
         for (int j = 0; j < 2; ++j) {
           const int leaf = 2 * pr + j;
           uint32_t v[2];
-          sample2(p, h[2 * j], h[2 * j + 1].w0, v);
+          sample2(p, div, h[2 * j], h[2 * j + 1].w0, v);
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             if (e < p.nl) {
-              const uint32_t n = p.div[e].n;
+              const uint32_t n = div[e].n;
               uint32_t r = v[e];
               if (tl[leaf]) r = mod_add(r, corr[e], n);          // int_mod_n.h:116-120
               if (party == 1) r = r == 0 ? 0u : n - r;            // int_mod_n.h:208-218
