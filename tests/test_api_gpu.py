@@ -150,6 +150,20 @@ def test_bit_exact_vs_oracle_evaluate_at(levels):
                                   O.evaluate_at(P, ok0, h, pts))
 
 
+# Small calls move no data by DMA by default: argument images of <= 128 KiB
+# are read by the kernels from page-locked memory and results of <= 1 MiB are
+# written there (PackedUploads / PinnedOut).  Every combination of those two
+# and the copying paths they replace stays bit-exact against the oracle.
+@pytest.mark.parametrize("upload", ["1", "0"])
+@pytest.mark.parametrize("output", ["1", "0"])
+@pytest.mark.parametrize("levels", [PARITY_CASES[0], PARITY_CASES[-1]], ids=str)
+def test_small_call_copy_modes(levels, upload, output, monkeypatch):
+    monkeypatch.setenv("DPF_UPLOAD_ZERO_COPY", upload)
+    monkeypatch.setenv("DPF_OUTPUT_ZERO_COPY", output)
+    test_bit_exact_vs_oracle_incremental(levels)
+    test_bit_exact_vs_oracle_evaluate_at(levels)
+
+
 def test_golden_full_domain_fixtures():
     g = json.load(open(os.path.join(GOLDEN, "full_domain.json")))
     for case in g["cases"]:

@@ -39,8 +39,12 @@ def test_dcf_all_points_bit_exact(vt, n):
                 assert total[x] == (beta if x < alpha else [0] * len(beta)), (alpha, x)
 
 
-def test_dcf_uint64_large_domain():
-    # test.cc:125-177
+@pytest.mark.parametrize("upload,output", [("1", "1"), ("0", "0"), ("1", "0"), ("0", "1")])
+def test_dcf_uint64_large_domain(upload, output, monkeypatch):
+    # test.cc:125-177; with and without the small-call zero-copy paths
+    # (DPF_UPLOAD_ZERO_COPY / DPF_OUTPUT_ZERO_COPY).
+    monkeypatch.setenv("DPF_UPLOAD_ZERO_COPY", upload)
+    monkeypatch.setenv("DPF_OUTPUT_ZERO_COPY", output)
     dcf = make(("int", 64), 64)
     P = O.dcf_params(64, ("int", 64))
     alpha = 50
