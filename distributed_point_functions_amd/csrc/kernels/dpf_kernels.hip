@@ -1017,6 +1017,14 @@ bool points_quad_on() {
   const char* v = std::getenv("DPF_POINTS_QUAD");
   return !(v && v[0] == '0');
 }
+// Launches of at most this many points run in latency mode: num_cus x 64 by
+// default (a wave per CU of one-lane chains); DPF_POINTS_QUAD_MAX=<points>
+// (read per launch) moves the cut-over (A/B hook).
+int64_t points_quad_max() {
+  const char* v = std::getenv("DPF_POINTS_QUAD_MAX");
+  const long long m = v && *v ? std::strtoll(v, nullptr, 10) : 0;
+  return m > 0 ? (int64_t)m : (int64_t)num_cus() * 64;
+}
 
 // DPF_POINTS_ILP=2|4 (read per launch) forces two or four chains per lane
 // (four only where a quarter of a key's points is a whole number of waves);
@@ -1052,7 +1060,7 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
   if constexpr (!SUM) {
     // At most a wave per CU of points: latency-bound, one lane quad per point.
     const int64_t points = pp.num_keys * pp.points_per_key;
-    if (FAST && points <= (int64_t)num_cus() * 64 && points_ilp() == 0 && points_quad_on()) {
+    if (FAST && points <= points_quad_max() && points_ilp() == 0 && points_quad_on()) {
       g_last_points_kernel = "points/quad";
       PointParams p = pp;
       p.num_items = points;
