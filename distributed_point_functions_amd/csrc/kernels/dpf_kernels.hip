@@ -1017,13 +1017,16 @@ bool points_quad_on() {
   const char* v = std::getenv("DPF_POINTS_QUAD");
   return !(v && v[0] == '0');
 }
-// Launches of at most this many points run in latency mode: num_cus x 64 by
-// default (a wave per CU of one-lane chains); DPF_POINTS_QUAD_MAX=<points>
-// (read per launch) moves the cut-over (A/B hook).
+// Launches of at most this many points run in latency mode: num_cus x 256 by
+// default, i.e. as many lane quads as one pass of 1024-thread workgroups on
+// every CU holds.  BatchEvaluation/10/40000 (40000 points per call) 2.54-2.63
+// -> 1.46-1.58 ms; /1/400000 stays on the lane chains (the quads would loop:
+// 1.01-1.17 vs 0.97-1.00 ms); profiles/r15_ab.txt part 19.
+// DPF_POINTS_QUAD_MAX=<points> (read per launch) moves the cut-over (A/B hook).
 int64_t points_quad_max() {
   const char* v = std::getenv("DPF_POINTS_QUAD_MAX");
   const long long m = v && *v ? std::strtoll(v, nullptr, 10) : 0;
-  return m > 0 ? (int64_t)m : (int64_t)num_cus() * 64;
+  return m > 0 ? (int64_t)m : (int64_t)num_cus() * 256;
 }
 
 // DPF_POINTS_ILP=2|4 (read per launch) forces two or four chains per lane
@@ -1058,7 +1061,7 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
     }
   }
   if constexpr (!SUM) {
-    // At most a wave per CU of points: latency-bound, one lane quad per point.
+    // Up to one pass of lane quads over every CU: one lane quad per point.
     const int64_t points = pp.num_keys * pp.points_per_key;
     if (FAST && points <= points_quad_max() && points_ilp() == 0 && points_quad_on()) {
       g_last_points_kernel = "points/quad";

@@ -230,8 +230,8 @@ def test_points_kernel_chains_per_lane(levels, n_keys, ppk, ilp, monkeypatch):
 
 def test_points_kernel_default_dispatch():
     """Without the hook, a launch that fills every CU with 1024-thread
-    workgroups takes four chains per lane; a smaller one takes two (and one
-    below a wave of point pairs per CU)."""
+    workgroups takes four chains per lane; a smaller one takes two; one of at
+    most num_cus x 256 points runs one lane quad per point."""
     import torch
     from distributed_point_functions_amd import hip_abi as H
     levels = [(64, ("int", 64), 0)]
@@ -245,12 +245,25 @@ def test_points_kernel_default_dispatch():
     got = out.cpu().numpy().reshape(1024, 1024, 8)
     for k in (0, 1, 511, 1023):
         np.testing.assert_array_equal(got[k], O.evaluate_at(P, oks[k], 0, pts), err_msg=f"key {k}")
-    # 128 keys x 256 points: a wave per CU of point pairs, not a full chip of quads.
+    # 512 keys x 256 points: more than one pass of lane quads over the chip
+    # (num_cus x 256 points), less than a full chip of four-chain lanes.
+    mid = torch.empty(512 * 256 * 8, dtype=torch.uint8, device="cuda")
+    sub = dpf.upload_key_batch(batch, 0, 512)
+    dpf.evaluate_at_batch_to_device(sub, 0, _dev_points(pts[:256]), 256, mid, shared_points=True)
+    torch.cuda.synchronize()
+    assert H.last_points_kernel() == "points/ilp2"
+    got = mid.cpu().numpy().reshape(512, 256, 8)
+    for k in (0, 511):
+        np.testing.assert_array_equal(got[k], O.evaluate_at(P, oks[k], 0, pts[:256]), err_msg=f"key {k}")
+    # 128 keys x 256 points: within one pass of quads, latency mode.
     small = torch.empty(128 * 256 * 8, dtype=torch.uint8, device="cuda")
     sub = dpf.upload_key_batch(batch, 0, 128)
     dpf.evaluate_at_batch_to_device(sub, 0, _dev_points(pts[:256]), 256, small, shared_points=True)
     torch.cuda.synchronize()
-    assert H.last_points_kernel() == "points/ilp2"
+    assert H.last_points_kernel() == "points/quad"
+    got = small.cpu().numpy().reshape(128, 256, 8)
+    for k in (0, 127):
+        np.testing.assert_array_equal(got[k], O.evaluate_at(P, oks[k], 0, pts[:256]), err_msg=f"key {k}")
 
 
 QUAD_CASES = [
@@ -266,7 +279,7 @@ QUAD_CASES = [
 @pytest.mark.parametrize("quad", ["1", "0"])
 @pytest.mark.parametrize("levels,n_keys,ppk", QUAD_CASES, ids=str)
 def test_points_latency_mode(levels, n_keys, ppk, quad, monkeypatch):
-    """Small integer point evaluations (at most a wave of points per CU) run
+    """Small integer point evaluations (at most num_cus x 256 points) run
     one (key, point) per lane quad, lane c computing AES column c
     (eval_points_quad_kernel); DPF_POINTS_QUAD=0 keeps one chain per lane.
     Per-key and shared points equal the oracle either way."""
