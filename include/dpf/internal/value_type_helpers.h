@@ -347,7 +347,8 @@ HostSink VectorSink(std::vector<T>* out) {
   };
   s.grow = [out](size_t bytes) { GrowZeroed(out, (bytes + sizeof(T) - 1) / sizeof(T)); };
   s.chunk = [out](const uint8_t* src, size_t offset, size_t len) {
-    GrowZeroed(out, (offset + len) / sizeof(T));
+    // (Already grown when CopyToHostSink grew the whole result up front.)
+    if (out->size() < (offset + len) / sizeof(T)) GrowZeroed(out, (offset + len) / sizeof(T));
     uint8_t* dst = reinterpret_cast<uint8_t*>(out->data()) + offset;
     ParallelRanges(static_cast<int64_t>(len), int64_t{2} << 20, [&](int64_t lo, int64_t hi) {
       std::memcpy(dst + lo, src + lo, static_cast<size_t>(hi - lo));
@@ -389,11 +390,16 @@ HostSink UnpackSink(const std::vector<FlatValueType>* flats, int h, std::vector<
     ReserveOutputVector(*out, static_cast<int64_t>(bytes / (*flats)[h].packed_size), false);
     return nullptr;
   };
+  // Value-initialises the whole result (CopyToHostSink runs it on a helper
+  // thread while the DMA of the first chunk is in flight).
+  s.grow = [flats, h, out](size_t bytes) {
+    out->resize(bytes / static_cast<size_t>((*flats)[h].packed_size));
+  };
   s.chunk = [flats, h, out](const uint8_t* src, size_t offset, size_t len) {
     const FlatValueType& flat = (*flats)[h];
     const int64_t first = static_cast<int64_t>(offset / flat.packed_size);
     const int64_t cnt = static_cast<int64_t>(len / flat.packed_size);
-    out->resize(first + cnt);
+    if (static_cast<int64_t>(out->size()) < first + cnt) out->resize(first + cnt);
     UnpackInto<T>(flat, src, cnt, out->data() + first);
   };
   // Valid levels only (the sink is used after validation); 1 otherwise.
