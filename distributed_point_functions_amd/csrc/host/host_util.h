@@ -67,18 +67,18 @@ class PartEvents {
   std::vector<size_t> ends_;
 };
 
-// Results of kOverlapGrowMin..kOverlapGrowMax bytes that arrive through the
-// staging buffers are value-initialised on a helper thread during the DMA
-// (CopyToHostSink): one staging chunk (16 MiB), so nothing else overlaps
-// that DMA.  Larger results already overlap each chunk's growth and copy
-// with the next chunk's DMA, and growing them whole first measured slower
-// (uint128/22 7.4 -> 9.7 ms); below 4 MiB a thread costs about what it saves.
-// Measured: uint64/20 466 -> 364 us, uint128/20 845 -> 646 us,
-// Tuple<uint32_t x5>/20 1.46 -> 1.03 ms (profiles/r15_ab.txt part 20).
-// DPF_OVERLAP_GROW=0 (read per call) grows them chunk by chunk as before
-// (A/B and test hook).
+// Results of kOverlapGrowMin bytes up to below kOverlapGrowLimit that arrive
+// through the staging buffers are value-initialised on a helper thread
+// during the DMA (CopyToHostSink).  Measured: uint64/20 466 -> 364 us,
+// uint128/20 845 -> 646 us, Tuple<uint32_t x5>/20 (20 MiB) 1.46 -> 1.03 ms
+// (profiles/r15_ab.txt part 20).  From 32 MiB, glibc hands out fresh mmap
+// pages, whose faults the helper would take alone and ahead of every copy,
+// where chunk by chunk they overlap the next chunk's DMA (uint128/22
+// 7.4 -> 9.7 ms grown whole); below 4 MiB a thread costs about what it
+// saves.  DPF_OVERLAP_GROW=0 (read per call) grows them chunk by chunk as
+// before (A/B and test hook).
 constexpr size_t kOverlapGrowMin = size_t{4} << 20;
-constexpr size_t kOverlapGrowMax = size_t{16} << 20;
+constexpr size_t kOverlapGrowLimit = size_t{32} << 20;
 inline bool OverlapGrowOn() {
   const char* v = std::getenv("DPF_OVERLAP_GROW");
   return !(v && v[0] == '0');
@@ -95,7 +95,7 @@ inline int CopyToHostSink(const HostSink& sink, void* dst, const void* src, size
     auto consume = [](void* ctx, const void* chunk, size_t offset, size_t len) {
       (*static_cast<const HostSink*>(ctx)).chunk(static_cast<const uint8_t*>(chunk), offset, len);
     };
-    if (sink.grow && bytes >= kOverlapGrowMin && bytes <= kOverlapGrowMax && OverlapGrowOn()) {
+    if (sink.grow && bytes >= kOverlapGrowMin && bytes < kOverlapGrowLimit && OverlapGrowOn()) {
       // The result's one-thread value-initialisation (~60 GB/s) runs on a
       // helper thread while the first chunk's DMA is in flight; the chunks
       // are then copied (or unpacked) into the grown result in parallel.
