@@ -289,22 +289,6 @@ StatusOr<std::vector<uint128>> DistributedPointFunction::ValueCorrectionLeaves(c
 }
 
 namespace {
-// Uploads the correction words [start, stop) of `key` to device buffers.
-Status UploadCorrectionWords(const DpfKey& key, int start, int stop,
-                             dpf_internal::DeviceScratch* s, void* stream) {
-  const int L = stop - start;
-  std::vector<dpf_block> seeds(std::max(L, 1));
-  std::vector<uint8_t> cl(std::max(L, 1)), cr(std::max(L, 1));
-  for (int j = 0; j < L; ++j) {
-    const CorrectionWord& cw = key.correction_words(start + j);
-    seeds[j] = ToBlock(FromProtoBlock(cw.seed()));
-    cl[j] = cw.control_left();
-    cr[j] = cw.control_right();
-  }
-  DPF_RETURN_IF_ERROR(s->Upload(s->cw_seed, seeds.data(), seeds.size(), stream));
-  DPF_RETURN_IF_ERROR(s->Upload(s->cw_left, cl.data(), cl.size(), stream));
-  return s->Upload(s->cw_right, cr.data(), cr.size(), stream);
-}
 
 // Correction words [start, stop) of `key` added to a packed upload.
 struct PackedCws {
@@ -335,8 +319,20 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   const int64_t n = static_cast<int64_t>(prefixes.size());
   int start_level = hierarchy_to_tree()[ctx.partial_evaluations_level()];
   const int stop_level = hierarchy_to_tree()[hierarchy_level];
-  std::vector<dpf_block> seeds(std::max<int64_t>(n, 1));
-  std::vector<uint8_t> ctrl(std::max<int64_t>(n, 1));
+  auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
+  // The walk's inputs -- start seeds, control bits, paths, correction words --
+  // go up as ONE packed image (read in place by the kernel when small); the
+  // start seeds and control bits are written straight into it.
+  PackedUploads& pu = s->packed_pe;
+  DPF_RETURN_IF_ERROR(pu.Reset());
+  const int max_levels = std::max(stop_level - start_level, stop_level);
+  pu.Prepare(static_cast<size_t>(std::max<int64_t>(n, 1)) * (2 * sizeof(dpf_block) + 1) +
+             static_cast<size_t>(max_levels + 1) * (sizeof(dpf_block) + 2) + 6 * 256);
+  size_t o_seed, o_ctrl, o_paths;
+  dpf_block* seeds = pu.Reserve<dpf_block>(std::max<int64_t>(n, 1), &o_seed);
+  uint8_t* ctrl = pu.Reserve<uint8_t>(std::max<int64_t>(n, 1), &o_ctrl);
+  dpf_block* paths = pu.Reserve<dpf_block>(std::max<int64_t>(n, 1), &o_paths);
   if (ctx.partial_evaluations_size() > 0 && start_level <= stop_level) {
     const int shift = stop_level - start_level;
     auto parent_of = [&](int64_t i) -> uint128 { return shift < 128 ? prefixes[i] >> shift : 0; };
@@ -407,34 +403,41 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     }
   } else {
     const dpf_block root = ToBlock(FromProtoBlock(ctx.key().seed()));
+    const uint8_t party = static_cast<uint8_t>(ctx.key().party() & 1);
     for (int64_t i = 0; i < n; ++i) {
       seeds[i] = root;
-      ctrl[i] = static_cast<uint8_t>(ctx.key().party() & 1);
+      ctrl[i] = party;
     }
     start_level = 0;
   }
   // Everything that can fail on the host is checked before device work starts.
   if (before_device) DPF_RETURN_IF_ERROR(before_device());
-  auto* s = scratch_.get();
-  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
-  std::vector<dpf_block> paths(std::max<int64_t>(n, 1));
   dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) paths[i] = ToBlock(prefixes[i]);
   });
-  DPF_RETURN_IF_ERROR(s->Upload(s->path_seed, seeds.data(), seeds.size(), stream));
-  DPF_RETURN_IF_ERROR(s->Upload(s->path_ctrl, ctrl.data(), ctrl.size(), stream));
-  DPF_RETURN_IF_ERROR(s->Upload(s->paths, paths.data(), paths.size(), stream));
-  DPF_RETURN_IF_ERROR(UploadCorrectionWords(ctx.key(), start_level, stop_level, s, stream));
+  const PackedCws o_cw = AddCorrectionWords(ctx.key(), start_level, stop_level, pu);
+  DPF_RETURN_IF_ERROR(pu.Commit(stream));
+  dpf_block* dev_seed = pu.Ptr<dpf_block>(o_seed);
+  uint8_t* dev_ctrl = pu.Ptr<uint8_t>(o_ctrl);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight);
   HIP_RETURN_IF_ERROR(dpf_hip_eval_paths(
-      n, stop_level - start_level, s->path_seed.as<dpf_block>(), s->path_ctrl.as<uint8_t>(),
-      s->paths.as<dpf_block>(), s->cw_seed.as<dpf_block>(), s->cw_left.as<uint8_t>(),
-      s->cw_right.as<uint8_t>(), &kl, &kr, s->path_seed.as<dpf_block>(), s->path_ctrl.as<uint8_t>(),
-      stream));
+      n, stop_level - start_level, dev_seed, dev_ctrl, pu.Ptr<dpf_block>(o_paths),
+      pu.Ptr<dpf_block>(o_cw.seed), pu.Ptr<uint8_t>(o_cw.left), pu.Ptr<uint8_t>(o_cw.right), &kl,
+      &kr, dev_seed, dev_ctrl, stream));
+  // Whatever reads the walked seeds later (the caller's expansion) is
+  // ordered after this on `stream`; the caller marks the image used again
+  // after its launches (MarkStartUsed) so the next call waits for them too.
+  DPF_RETURN_IF_ERROR(pu.MarkUsed(stream));
   ctx.clear_partial_evaluations();
   if (update_ctx) {
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds.data(), s->path_seed.get(), n * sizeof(dpf_block), stream));
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(ctrl.data(), s->path_ctrl.get(), n, stream));
+    // The walked seeds and control bits back into the host image (in place
+    // when the kernel wrote them there), then into the context.
+    const size_t span = o_ctrl + static_cast<size_t>(n) - o_seed;
+    if (pu.zero_copy()) {
+      HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(stream));
+    } else {
+      HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds, dev_seed, span, stream));
+    }
     auto& pes = ctx.mutable_partial_evaluations()->vec();
     pes.resize(n);
     dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
@@ -448,8 +451,8 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   }
   ctx.set_partial_evaluations_level(hierarchy_level);
   out->n = n;
-  out->seeds = s->path_seed.as<dpf_block>();
-  out->ctrl = s->path_ctrl.as<uint8_t>();
+  out->seeds = dev_seed;
+  out->ctrl = dev_ctrl;
   return OkStatus();
 }
 
@@ -545,10 +548,20 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   const int previous_hierarchy_level = ctx.previous_hierarchy_level();
   if (!prefixes.empty()) {
     previous_log_domain_size = parameters()[previous_hierarchy_level].log_domain_size();
-    for (uint128 prefix : prefixes) {
-      if (previous_log_domain_size < 128 &&
-          prefix >= (static_cast<uint128>(1) << previous_log_domain_size))
-        return InvalidArgumentError("Index " + Uint128ToString(prefix) +
+    if (previous_log_domain_size < 128) {
+      // The first out-of-range prefix is the one reported, as the reference's
+      // loop does; the scan runs on host threads.
+      const uint128 limit = static_cast<uint128>(1) << previous_log_domain_size;
+      const int64_t np = static_cast<int64_t>(prefixes.size());
+      const int chunks = dpf_internal::NumChunks(np);
+      std::vector<int64_t> first_bad(chunks, np);
+      dpf_internal::ParallelChunks(np, chunks, [&](int c, int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i)
+          if (prefixes[i] >= limit) { first_bad[c] = i; return; }
+      });
+      const int64_t bad = *std::min_element(first_bad.begin(), first_bad.end());
+      if (bad < np)
+        return InvalidArgumentError("Index " + Uint128ToString(prefixes[bad]) +
                                     " out of range for hierarchy level " +
                                     std::to_string(previous_hierarchy_level));
     }
@@ -712,6 +725,9 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
                                        stream));
   }
   DPF_RETURN_IF_ERROR(up.MarkUsed(stream));
+  // The expansion read its start seeds out of the walk's image: the next
+  // call's ComputePartialEvaluations must not rewrite it before that is done.
+  if (!tree_indices.empty()) DPF_RETURN_IF_ERROR(s->packed_pe.MarkUsed(stream));
   void* result = expand_out;
   if (!identity) {
     std::vector<int64_t> offsets(num_prefixes);
@@ -1000,6 +1016,7 @@ Status DistributedPointFunction::EvaluateAtToHost(const DpfKey& key, int hierarc
       up.Ptr<int32_t>(o_bi), up.Ptr<dpf_block>(o_cw.seed), up.Ptr<uint8_t>(o_cw.left),
       up.Ptr<uint8_t>(o_cw.right), &kl, &kr, &kv, &desc, up.Ptr<dpf_block>(o_vcw), out, nullptr));
   DPF_RETURN_IF_ERROR(up.MarkUsed(nullptr));
+  if (ctx) DPF_RETURN_IF_ERROR(s->packed_pe.MarkUsed(nullptr));   // start seeds read from it
   clk.mark(3);
   if (g_until_timing_on) {
     HIP_RETURN_IF_ERROR(dpf_hip_stream_sync(nullptr));

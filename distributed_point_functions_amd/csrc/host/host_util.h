@@ -493,6 +493,8 @@ class PackedUploads {
     return reinterpret_cast<T*>((zero_copy_ ? static_cast<char*>(pinned_)
                                             : static_cast<char*>(arena_.get())) + off);
   }
+  // True when this call's kernels read (and write) the host image itself.
+  bool zero_copy() const { return zero_copy_; }
 
  private:
   static constexpr size_t kMaxPinned = size_t{64} << 20;
@@ -640,9 +642,8 @@ class DeviceScratch {
  public:
   std::recursive_mutex mu;
   PackedUploads packed;
-  DeviceBuffer start_seed, start_ctrl, paths, path_seed, path_ctrl;
-  DeviceBuffer cw_seed, cw_left, cw_right, vcw, out, gathered, offsets;
-  DeviceBuffer key_seed, party, block_index, workspace;
+  PackedUploads packed_pe;   // ComputePartialEvaluations' walk (its seeds feed the expansion)
+  DeviceBuffer out, gathered, offsets, party, workspace;
   StreamFence workspace_fence;  // the sum kernels' 192-bit accumulators
   HostStaging staging;
   PinnedOut small_out;           // results of small calls, written by the kernels
