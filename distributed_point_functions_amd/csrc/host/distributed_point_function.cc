@@ -586,19 +586,23 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
       return InvalidArgumentError("device output buffer too small");
   }
 
+  auto* s = scratch_.get();
+  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   // Unique tree indices of the prefixes, in first-seen order (h:718-742).
-  std::vector<uint128> tree_indices;
-  std::vector<std::pair<int64_t, int>> prefix_map;
-  if (num_prefixes > 0)
+  std::vector<uint128>& tree_indices = s->tree_indices;
+  std::vector<std::pair<int64_t, int>>& prefix_map = s->prefix_map;
+  if (num_prefixes > 0) {
     dpf_internal::DedupTreeIndices(prefixes,
                                    parameters()[previous_hierarchy_level].log_domain_size() -
                                        hierarchy_to_tree()[previous_hierarchy_level],
                                    &tree_indices, &prefix_map);
+  } else {
+    tree_indices.clear();
+    prefix_map.clear();
+  }
 
   // ExpandAndUpdateContext (cc:455-498): starting seeds on the device.  The
   // value correction of this level (h:761-780) is parsed before device work.
-  auto* s = scratch_.get();
-  std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   clk.count_call();
   clk.mark(0);
   std::vector<uint128> vcw;
@@ -678,8 +682,15 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   if (num_prefixes > 0) {
     identity = (outputs_per_prefix == blocks_per_tree_prefix * cepb) &&
                static_cast<int64_t>(tree_indices.size()) == num_prefixes;
-    for (int64_t i = 0; identity && i < num_prefixes; ++i)
-      identity = prefix_map[i].first == i && prefix_map[i].second == 0;
+    if (identity) {
+      const int chunks = dpf_internal::NumChunks(num_prefixes);
+      std::vector<char> ok(chunks, 1);
+      dpf_internal::ParallelChunks(num_prefixes, chunks, [&](int c, int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i)
+          if (prefix_map[i].first != i || prefix_map[i].second != 0) { ok[c] = 0; return; }
+      });
+      identity = std::all_of(ok.begin(), ok.end(), [](char x) { return x != 0; });
+    }
   }
   // A small host result is written by the kernels straight into page-locked
   // memory (PinnedOut): no D2H copy.
@@ -731,9 +742,11 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
   void* result = expand_out;
   if (!identity) {
     std::vector<int64_t> offsets(num_prefixes);
-    for (int64_t i = 0; i < num_prefixes; ++i)
-      offsets[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
-                   prefix_map[i].second * outputs_per_prefix;
+    dpf_internal::ParallelFor(num_prefixes, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i)
+        offsets[i] = prefix_map[i].first * blocks_per_tree_prefix * cepb +
+                     prefix_map[i].second * outputs_per_prefix;
+    });
     DPF_RETURN_IF_ERROR(s->Upload(s->offsets, offsets.data(), offsets.size(), stream));
     if (device_out) {
       if (capacity_bytes < total * esz) return InvalidArgumentError("device output buffer too small");

@@ -250,9 +250,11 @@ void ParallelChunks(int64_t n, int chunks, F fn) {
 inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<uint128>* tree_indices,
                              std::vector<std::pair<int64_t, int>>* prefix_map) {
   const int64_t P = static_cast<int64_t>(prefixes.size());
-  tree_indices->clear();
-  prefix_map->clear();
-  if (P == 0) return;
+  if (P == 0) {
+    tree_indices->clear();
+    prefix_map->clear();
+    return;
+  }
   const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
   const int chunks = NumChunks(P);
   std::vector<char> chunk_ascending(chunks, 1);
@@ -277,6 +279,8 @@ inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<
       first[c + 1] = k;
     });
     for (int c = 0; c < chunks; ++c) first[c + 1] += first[c];
+    // Every element is overwritten below: vectors kept from an earlier call
+    // (the caller's scratch) only value-initialise what they grow by.
     tree_indices->resize(first[chunks]);
     prefix_map->resize(P);
     ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
@@ -290,6 +294,8 @@ inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<
   }
   std::unordered_map<uint128, int64_t, U128Hash> inverse;
   inverse.reserve(P * 2);
+  tree_indices->clear();
+  prefix_map->clear();
   tree_indices->reserve(P);
   prefix_map->reserve(P);
   for (int64_t i = 0; i < P; ++i) {
@@ -592,7 +598,9 @@ class StreamFence {
 
 // Page-locked memory for the result of a small call (<= 1 MiB): the kernel
 // writes it over PCIe and the host reads it after a stream sync -- no D2H
-// DMA and its ~5 us of latency (profiles/r13_latency_microbench.txt).
+// DMA and its ~5 us of latency (profiles/r13_latency_microbench.txt).  One
+// 1 MiB buffer per DistributedPointFunction / DistributedComparisonFunction
+// object, allocated at its first small call and freed with the object.
 // DPF_OUTPUT_ZERO_COPY=0 (read per call) turns it off (A/B and test hook).
 class PinnedOut {
  public:
@@ -643,6 +651,10 @@ class DeviceScratch {
   std::recursive_mutex mu;
   PackedUploads packed;
   PackedUploads packed_pe;   // ComputePartialEvaluations' walk (its seeds feed the expansion)
+  // EvaluateUntil's prefix dedup, kept across calls so a call of the same
+  // size value-initialises nothing.
+  std::vector<uint128> tree_indices;
+  std::vector<std::pair<int64_t, int>> prefix_map;
   DeviceBuffer out, gathered, offsets, party, workspace;
   StreamFence workspace_fence;  // the sum kernels' 192-bit accumulators
   HostStaging staging;
