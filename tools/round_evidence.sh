@@ -66,7 +66,7 @@ part3)
   ;;
 part4)
   PROFILE_PASS_LIMIT=400 profline heavy_hitters "hh_level_kernel|batch_level_kernel<Mod32V<2, true>, 2, true>|gather_seeds_kernel|finalize_sums_kernel" total:2 heavy_hitters "--no-cpu-baseline" --workload heavy_hitters
-  line config1 --log-domain 20 --steps 500 --warmup 50
+  line config1 --log-domain 20 --steps 2000 --warmup 5000   # ~0.3 s of warmup: the GPU at full clock
   line syn_dev32 --workload synthetic_hierarchical_device --domain 32
   line syn_dev128 --workload synthetic_hierarchical_device --domain 128
   line syn_h32 --workload synthetic_hierarchical --domain 32
