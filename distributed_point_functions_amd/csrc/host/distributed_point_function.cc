@@ -343,7 +343,9 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     // merge passes on host threads instead of a hash map, with the
     // reference's duplicate check (cc:365-383) on adjacent equal prefixes and
     // its lookup error (cc:392-407).
-    std::vector<uint128> stored(m);
+    // Kept in the object's scratch: a call of the same size value-initialises nothing.
+    std::vector<uint128>& stored = s->stored_prefixes;
+    stored.resize(m);
     dpf_internal::ParallelFor(m, [&](int64_t lo, int64_t hi) {
       for (int64_t j = lo; j < hi; ++j) stored[j] = FromProtoBlock(pe[j].prefix());
     });
@@ -360,12 +362,19 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     bool sorted = std::all_of(ok_m.begin(), ok_m.end(), [](char x) { return x != 0; }) &&
                   std::all_of(ok_n.begin(), ok_n.end(), [](char x) { return x != 0; });
     if (sorted) {
-      for (int64_t j = 1; j < m; ++j)
-        if (stored[j - 1] == stored[j] &&
-            (FromProtoBlock(pe[j - 1].seed()) != FromProtoBlock(pe[j].seed()) ||
-             pe[j - 1].control_bit() != pe[j].control_bit()))
-          return InvalidArgumentError(
-              "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
+      std::vector<char> dup_ok(chunks_m, 1);
+      dpf_internal::ParallelChunks(m, chunks_m, [&](int c, int64_t lo, int64_t hi) {
+        for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
+          if (stored[j - 1] == stored[j] &&
+              (FromProtoBlock(pe[j - 1].seed()) != FromProtoBlock(pe[j].seed()) ||
+               pe[j - 1].control_bit() != pe[j].control_bit())) {
+            dup_ok[c] = 0;
+            return;
+          }
+      });
+      if (!std::all_of(dup_ok.begin(), dup_ok.end(), [](char x) { return x != 0; }))
+        return InvalidArgumentError(
+            "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
       std::vector<char> missing(chunks_n, 0);
       dpf_internal::ParallelChunks(n, chunks_n, [&](int c, int64_t lo, int64_t hi) {
         int64_t j = std::lower_bound(stored.begin(), stored.end(), parent_of(lo)) - stored.begin();
@@ -428,7 +437,7 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   // ordered after this on `stream`; the caller marks the image used again
   // after its launches (MarkStartUsed) so the next call waits for them too.
   DPF_RETURN_IF_ERROR(pu.MarkUsed(stream));
-  ctx.clear_partial_evaluations();
+  if (!update_ctx) ctx.clear_partial_evaluations();
   if (update_ctx) {
     // The walked seeds and control bits back into the host image (in place
     // when the kernel wrote them there), then into the context.
@@ -438,6 +447,8 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     } else {
       HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds, dev_seed, span, stream));
     }
+    // Resized, not cleared first: a context whose previous level stored as
+    // many partial evaluations constructs none, and every field is rewritten.
     auto& pes = ctx.mutable_partial_evaluations()->vec();
     pes.resize(n);
     dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
@@ -480,10 +491,10 @@ struct UntilTiming {
     if (calls > 100 && std::getenv("DPF_HOST_TIMING"))
       std::fprintf(stderr,
                    "[EvaluateUntil host timing] calls=%ld per call: validate=%.2fus "
-                   "reset+vcw=%.2fus pack=%.2fus commit=%.2fus launch=%.2fus reserve=%.2fus "
-                   "copy=%.2fus\n",
-                   calls, t[0] * 1e6 / n, t[5] * 1e6 / n, t[6] * 1e6 / n, t[1] * 1e6 / n,
-                   t[2] * 1e6 / n, t[3] * 1e6 / n, t[4] * 1e6 / n);
+                   "dedup=%.2fus walk+vcw=%.2fus pack=%.2fus commit=%.2fus launch=%.2fus "
+                   "reserve=%.2fus copy=%.2fus\n",
+                   calls, t[7] * 1e6 / n, t[0] * 1e6 / n, t[5] * 1e6 / n, t[6] * 1e6 / n,
+                   t[1] * 1e6 / n, t[2] * 1e6 / n, t[3] * 1e6 / n, t[4] * 1e6 / n);
   }
 };
 UntilTiming g_until_timing;
@@ -586,6 +597,7 @@ Status DistributedPointFunction::EvaluateUntilCore(int hierarchy_level, Span<con
       return InvalidArgumentError("device output buffer too small");
   }
 
+  clk.mark(7);
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
   // Unique tree indices of the prefixes, in first-seen order (h:718-742).
