@@ -310,6 +310,42 @@ PackedCws AddCorrectionWords(const DpfKey& key, int start, int stop, PackedUploa
   o.right = up.Add(cr.data(), cr.size());
   return o;
 }
+
+// Phase split of the prefix walk (ComputePartialEvaluations), printed at exit
+// with DPF_HOST_TIMING: the lookup of the stored evaluations, the image and
+// its upload, the walk on the device (with the walked seeds' D2H), and the
+// context rewrite.
+struct WalkTiming {
+  double t[4] = {0, 0, 0, 0};
+  long calls = 0;
+  ~WalkTiming() {
+    if (calls > 0 && std::getenv("DPF_HOST_TIMING"))
+      std::fprintf(stderr,
+                   "[prefix walk host timing] calls=%ld per call: lookup=%.2fus upload=%.2fus "
+                   "device=%.2fus context=%.2fus\n",
+                   calls, t[0] * 1e6 / calls, t[1] * 1e6 / calls, t[2] * 1e6 / calls,
+                   t[3] * 1e6 / calls);
+  }
+};
+WalkTiming g_walk_timing;
+std::mutex g_walk_timing_mu;
+const bool g_walk_timing_on = std::getenv("DPF_HOST_TIMING") != nullptr;
+struct WalkClock {
+  std::chrono::steady_clock::time_point last = std::chrono::steady_clock::now();
+  double t[4] = {0, 0, 0, 0};
+  void mark(int phase) {
+    if (!g_walk_timing_on) return;
+    auto now = std::chrono::steady_clock::now();
+    t[phase] += std::chrono::duration<double>(now - last).count();
+    last = now;
+  }
+  ~WalkClock() {
+    if (!g_walk_timing_on) return;
+    std::lock_guard<std::mutex> lock(g_walk_timing_mu);
+    ++g_walk_timing.calls;
+    for (int i = 0; i < 4; ++i) g_walk_timing.t[i] += t[i];
+  }
+};
 }  // namespace
 
 Status DistributedPointFunction::ComputePartialEvaluations(
@@ -321,6 +357,7 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   const int stop_level = hierarchy_to_tree()[hierarchy_level];
   auto* s = scratch_.get();
   std::lock_guard<std::recursive_mutex> scratch_lock(s->mu);  // one call at a time per object
+  WalkClock wclk;
   // The walk's inputs -- start seeds, control bits, paths, correction words --
   // go up as ONE packed image (read in place by the kernel when small); the
   // start seeds and control bits are written straight into it.
@@ -339,53 +376,60 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     const auto& pe = ctx.partial_evaluations();
     const int64_t m = pe.size();
     // Sorted fast path (the usual hierarchical case: both the stored prefixes
-    // and the lookups come out of EvaluateUntil in ascending order): chunked
-    // merge passes on host threads instead of a hash map, with the
-    // reference's duplicate check (cc:365-383) on adjacent equal prefixes and
-    // its lookup error (cc:392-407).
-    // Kept in the object's scratch: a call of the same size value-initialises nothing.
-    std::vector<uint128>& stored = s->stored_prefixes;
-    stored.resize(m);
-    dpf_internal::ParallelFor(m, [&](int64_t lo, int64_t hi) {
-      for (int64_t j = lo; j < hi; ++j) stored[j] = FromProtoBlock(pe[j].prefix());
-    });
+    // and the lookups come out of EvaluateUntil in ascending order): two
+    // chunked passes on host threads instead of a hash map.  The first checks
+    // that the stored prefixes ascend and applies the reference's duplicate
+    // check (cc:365-383) to adjacent equal ones; the second checks that the
+    // lookups' parents ascend and merges them against the stored prefixes,
+    // with the reference's lookup error (cc:392-407).  Either order broken:
+    // the hash map below redoes the lookup.
+    auto stored_at = [&](int64_t j) -> uint128 { return FromProtoBlock(pe[j].prefix()); };
     const int chunks_m = dpf_internal::NumChunks(m), chunks_n = dpf_internal::NumChunks(n);
-    std::vector<char> ok_m(chunks_m, 1), ok_n(chunks_n, 1);
+    std::vector<char> ok_m(chunks_m, 1), dup_ok(chunks_m, 1);
     dpf_internal::ParallelChunks(m, chunks_m, [&](int c, int64_t lo, int64_t hi) {
-      for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
-        if (stored[j - 1] > stored[j]) { ok_m[c] = 0; return; }
+      if (lo >= hi) return;
+      const int64_t first = std::max<int64_t>(lo, 1);
+      uint128 prev = stored_at(first - 1);
+      for (int64_t j = first; j < hi; ++j) {
+        const uint128 cur = stored_at(j);
+        if (prev > cur) { ok_m[c] = 0; return; }
+        if (prev == cur && dup_ok[c] &&
+            (FromProtoBlock(pe[j - 1].seed()) != FromProtoBlock(pe[j].seed()) ||
+             pe[j - 1].control_bit() != pe[j].control_bit()))
+          dup_ok[c] = 0;
+        prev = cur;
+      }
     });
-    dpf_internal::ParallelChunks(n, chunks_n, [&](int c, int64_t lo, int64_t hi) {
-      for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
-        if (parent_of(i - 1) > parent_of(i)) { ok_n[c] = 0; return; }
-    });
-    bool sorted = std::all_of(ok_m.begin(), ok_m.end(), [](char x) { return x != 0; }) &&
-                  std::all_of(ok_n.begin(), ok_n.end(), [](char x) { return x != 0; });
+    auto all = [](const std::vector<char>& v) {
+      return std::all_of(v.begin(), v.end(), [](char x) { return x != 0; });
+    };
+    bool sorted = all(ok_m);
+    if (sorted && !all(dup_ok))
+      return InvalidArgumentError(
+          "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
+    std::vector<char> ok_n(chunks_n, 1), missing(chunks_n, 0);
     if (sorted) {
-      std::vector<char> dup_ok(chunks_m, 1);
-      dpf_internal::ParallelChunks(m, chunks_m, [&](int c, int64_t lo, int64_t hi) {
-        for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
-          if (stored[j - 1] == stored[j] &&
-              (FromProtoBlock(pe[j - 1].seed()) != FromProtoBlock(pe[j].seed()) ||
-               pe[j - 1].control_bit() != pe[j].control_bit())) {
-            dup_ok[c] = 0;
-            return;
-          }
-      });
-      if (!std::all_of(dup_ok.begin(), dup_ok.end(), [](char x) { return x != 0; }))
-        return InvalidArgumentError(
-            "Duplicate prefix in `ctx.partial_evaluations()` with mismatching seed or control bit");
-      std::vector<char> missing(chunks_n, 0);
       dpf_internal::ParallelChunks(n, chunks_n, [&](int c, int64_t lo, int64_t hi) {
-        int64_t j = std::lower_bound(stored.begin(), stored.end(), parent_of(lo)) - stored.begin();
+        if (lo >= hi) return;
+        int64_t j = std::partition_point(pe.begin(), pe.end(),
+                                         [&](const PartialEvaluation& e) {
+                                           return FromProtoBlock(e.prefix()) < parent_of(lo);
+                                         }) -
+                    pe.begin();
+        uint128 prev = lo > 0 ? parent_of(lo - 1) : 0;
         for (int64_t i = lo; i < hi; ++i) {
           const uint128 want = parent_of(i);
-          while (j < m && stored[j] < want) ++j;
-          if (j == m || stored[j] != want) { missing[c] = 1; return; }
+          if (want < prev) { ok_n[c] = 0; return; }
+          prev = want;
+          while (j < m && stored_at(j) < want) ++j;
+          if (j == m || stored_at(j) != want) { missing[c] = 1; return; }
           seeds[i] = ToBlock(FromProtoBlock(pe[j].seed()));
           ctrl[i] = pe[j].control_bit();
         }
       });
+      sorted = all(ok_n);
+    }
+    if (sorted) {
       if (std::any_of(missing.begin(), missing.end(), [](char x) { return x != 0; }))
         return InvalidArgumentError("Prefix not present in ctx.partial_evaluations at hierarchy level " +
                                     std::to_string(hierarchy_level));
@@ -421,11 +465,13 @@ Status DistributedPointFunction::ComputePartialEvaluations(
   }
   // Everything that can fail on the host is checked before device work starts.
   if (before_device) DPF_RETURN_IF_ERROR(before_device());
+  wclk.mark(0);
   dpf_internal::ParallelFor(n, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) paths[i] = ToBlock(prefixes[i]);
   });
   const PackedCws o_cw = AddCorrectionWords(ctx.key(), start_level, stop_level, pu);
   DPF_RETURN_IF_ERROR(pu.Commit(stream));
+  wclk.mark(1);
   dpf_block* dev_seed = pu.Ptr<dpf_block>(o_seed);
   uint8_t* dev_ctrl = pu.Ptr<uint8_t>(o_ctrl);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight);
@@ -447,6 +493,7 @@ Status DistributedPointFunction::ComputePartialEvaluations(
     } else {
       HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds, dev_seed, span, stream));
     }
+    wclk.mark(2);
     // Resized, not cleared first: a context whose previous level stored as
     // many partial evaluations constructs none, and every field is rewritten.
     auto& pes = ctx.mutable_partial_evaluations()->vec();
@@ -459,6 +506,7 @@ Status DistributedPointFunction::ComputePartialEvaluations(
         e->set_control_bit(ctrl[i] != 0);
       }
     });
+    wclk.mark(3);
   }
   ctx.set_partial_evaluations_level(hierarchy_level);
   out->n = n;

@@ -655,7 +655,6 @@ class DeviceScratch {
   // size value-initialises nothing.
   std::vector<uint128> tree_indices;
   std::vector<std::pair<int64_t, int>> prefix_map;
-  std::vector<uint128> stored_prefixes;   // ComputePartialEvaluations' lookup table
   DeviceBuffer out, gathered, offsets, party, workspace;
   StreamFence workspace_fence;  // the sum kernels' 192-bit accumulators
   HostStaging staging;
