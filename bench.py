@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Headline benchmark: full-domain DPF evaluation, 2^30 uint64 outputs per GPU.
+"""Headline benchmark: full-domain DPF evaluation of a 2^30-output uint64 domain.
 
 Metric (BASELINE.json): "DPF leaf evals/sec, full-domain 2^30 uint64 at
 1/2/4/8 GPUs; AES blocks/s" -- configs[1]: DpfParameters{log_domain_size=30,
@@ -16,17 +16,26 @@ Keys are generated on the CPU (out of scope for the GPU) before
 the timed region.  The PCIe-inclusive host-output rate (`--host-output`,
 below) is reported beside it, never as `value`.
 
-Multi-GPU (distributed_point_functions_amd/sharding.py): weak
-scaling by subtree prefix.  With N = 2^k ranks the domain is 2^(30 + k); rank r
+Multi-GPU (distributed_point_functions_amd/sharding.py): the
+metric's configuration is ONE 2^30-output domain at 1/2/4/8 GPUs, so the
+default is strong scaling by subtree prefix: with N = 2^k ranks, rank r
 path-walks the top k tree levels along the bits of r and expands its own
-2^30-output subtree.  No collective on the data path; one all_reduce(MAX) of
-the step time outside the timed region.
+2^(30-k)-output subtree; `value` = 2^30 outputs / the max-over-ranks step
+time.  `--scaling weak` keeps 2^30 outputs per GPU (domain 2^(30+k)); the
+uint128 workload (config 3: 2^34 outputs over 8 GPUs = 2^31 per GPU) is weak
+by default.  No collective on the data path; one all_reduce(MAX) of the step
+time outside the timed region.  `--rehearse-world W` runs, in one process on
+one GPU, exactly the shard rank 0 of a W-rank run evaluates (the per-rank
+kernel and fixed per-step host cost at that shard size).
 
-`--host-output` (configs 2 and 3) adds `api_level`: the reference's own call
-shape, EvaluateUntil<uint64_t / absl::uint128>(0, {}, ctx) returning a
-std::vector in host memory (the device kernel + a bounce-buffered D2H copy
-into the caller's vector), timed on the same key -- PCIe-inclusive, reported
-beside the kernel-level number and never as `value`.
+The line also carries, beside `value` and never in it:
+* `roofline.sustained_clock_ghz` / `clk_per_aes_per_cu`: the shader clock the
+  timed launches themselves ran at (s_memtime / s_memrealtime stamps of every
+  workgroup, dpf_hip_clock_probe), so a box can be told from a regression;
+* `api_level` (configs 2 and 3, N = 1; `--no-host-output` skips it): the
+  reference's own call shape, EvaluateUntil<uint64_t / absl::uint128>(0, {},
+  ctx) returning a std::vector in host memory (the device kernel + the D2H
+  copy into the caller's vector), timed on the same key -- PCIe-inclusive.
 
 Run: python bench.py [--gpus N --steps K --warmup W]
      python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -73,12 +82,21 @@ def parse():
                     help="timed steps (default 20; 1 for heavy_hitters, whose step is a full pass)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 3; 1)")
     ap.add_argument("--log-domain", type=int, default=LOG_PER_GPU,
-                    help="log2 outputs per GPU (default 30 = the BASELINE config)")
+                    help="log2 outputs: of the whole domain (strong scaling) or per GPU (weak); "
+                         "default 30 = the BASELINE config (31 per GPU for full_domain_u128)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--host-output", action="store_true",
-                    help="full_domain / full_domain_u128: also time the drop-in API call that "
-                         "returns host memory, EvaluateUntil<T>(0, {}, ctx) -> std::vector<T> "
-                         "(reported in `api_level`, never as `value`)")
+    ap.add_argument("--host-output", dest="host_output", action="store_true", default=True,
+                    help="full_domain / full_domain_u128 at N = 1 (default on): also time the "
+                         "drop-in API call that returns host memory, EvaluateUntil<T>(0, {}, ctx) "
+                         "-> std::vector<T> (reported in `api_level`, never as `value`)")
+    ap.add_argument("--no-host-output", dest="host_output", action="store_false")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                    help="full_domain*: strong = one 2^log-domain split over the N GPUs (default; "
+                         "the metric's configuration), weak = 2^log outputs per GPU (default for "
+                         "full_domain_u128, whose config 3 is 2^31 outputs per GPU x 8)")
+    ap.add_argument("--rehearse-world", type=int, default=None,
+                    help="full_domain*: one process evaluates the shard rank 0 of a W-rank run "
+                         "would (per-rank kernel time and fixed per-step cost at that size)")
     ap.add_argument("--host-output-reps", type=int, default=3)
     ap.add_argument("--cpu-chunks", type=int, default=32,
                     help="CPU baseline sample = this many 2^24-output subtrees of the same key")
@@ -108,6 +126,10 @@ def parse():
         args.steps = 1 if long_step else 20
     if args.warmup is None:
         args.warmup = 1 if long_step else 3
+    if args.scaling is None:
+        args.scaling = "weak" if args.workload == "full_domain_u128" else "strong"
+    if args.rehearse_world is not None and (args.gpus != 1 or not args.workload.startswith("full_domain")):
+        raise SystemExit("--rehearse-world runs one full_domain* process (--gpus 1)")
     return args
 
 
@@ -450,24 +472,38 @@ def init_ranks(torch, dist, gpus: int = None):
     the device for collective scalars (None: host tensors).  `gpus` (the
     --gpus flag) must equal the launcher's world size.
     DPF_BENCH_ONE_GPU=1 rehearses the N-rank path on a one-GPU box: every rank
-    on cuda:0, a gloo group (RCCL refuses two ranks on one device)."""
+    on cuda:0, a gloo group (RCCL refuses two ranks on one device).
+    DPF_BENCH_FORCE_PG=1 builds the RCCL group even for one rank, so every
+    collective of the N-rank path (the max-over-ranks timing, the share
+    all-reduce) runs through RCCL on a one-GPU box (tests/test_rccl_gpu.py)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if gpus is not None and world != gpus:
         raise SystemExit(f"--gpus {gpus} but {world} rank(s) running")
     one_gpu = os.environ.get("DPF_BENCH_ONE_GPU") == "1"
+    force = os.environ.get("DPF_BENCH_FORCE_PG") == "1"
     if one_gpu:
         local = 0
     coll = None
-    if world > 1:
+    if world > 1 or force:
         torch.cuda.set_device(local)
-        if one_gpu:
+        if world == 1:        # a one-rank group outside a launcher
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if one_gpu and world > 1:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             coll = torch.device("cuda", local)
     return world, rank, local, coll
+
+
+def group_up(dist) -> bool:
+    """A process group exists (N > 1, or one forced rank)."""
+    return dist.is_available() and dist.is_initialized()
 
 
 def main():
@@ -498,7 +534,11 @@ def main():
 
     bits = 128 if args.workload == "full_domain_u128" else 64
     esz = bits // 8
-    log_domain = S.weak_scaling_log_domain(args.log_domain, world)
+    # The partition: `shards` subtrees of which this process evaluates shard
+    # `shard` (rank r of N; shard 0 of W in a --rehearse-world W run).
+    shards, shard = (args.rehearse_world, 0) if args.rehearse_world else (world, rank)
+    log_domain = (S.weak_scaling_log_domain(args.log_domain, shards) if args.scaling == "weak"
+                  else args.log_domain)
     params = pb.DpfParameters()
     params.log_domain_size = log_domain
     if args.workload == "full_domain_tuple":
@@ -520,8 +560,8 @@ def main():
     key, _ = dpf.generate_keys_incremental(alpha, [beta], seeds=(0x243F6A8885A308D3,
                                                                  0x13198A2E03707344))
     ctx0 = dpf.create_evaluation_context(key)
-    depth = dpf.hierarchy_to_tree()[0] - S.shard_bits(world)   # tree levels expanded per rank
-    outputs_per_rank = 1 << args.log_domain
+    depth = dpf.hierarchy_to_tree()[0] - S.shard_bits(shards)   # tree levels expanded per rank
+    outputs_per_rank = 1 << S.strong_scaling_log_outputs(log_domain, shards)
     out = torch.empty(outputs_per_rank * esz, dtype=torch.uint8, device=dev)
 
     def step(evs=None):
@@ -529,7 +569,7 @@ def main():
         ctx.CopyFrom(ctx0)
         if evs is not None:
             evs[0].record(stream)
-        n = dpf.evaluate_shard_to_device(0, rank, world, ctx, out, stream=stream)
+        n = dpf.evaluate_shard_to_device(0, shard, shards, ctx, out, stream=stream)
         if evs is not None:
             evs[1].record(stream)
         return n
@@ -537,25 +577,29 @@ def main():
     for _ in range(args.warmup):
         assert step() == outputs_per_rank
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(H.Event(), H.Event()) for _ in range(args.steps)]
+    H.clock_probe(True)          # two s_memtime/s_memrealtime stamps per workgroup
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(evs[i])
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    if world > 1:
+    clock = H.clock_probe_read()
+    H.clock_probe(False)
+    if group_up(dist):
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
     kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
     ginfo = S.group_info(kern_ms, device=coll)
+    clocks = S.gather_over_ranks(clock["clock_ghz"], device=coll)
 
     # Spot-check the last step's output (sum of the two parties' shares is beta
     # at alpha, 0 elsewhere) on a few positions of this rank's shard.
-    _check_shard(dpf, key, out, rank, world, outputs_per_rank, alpha, bits)
+    _check_shard(dpf, key, out, shard, shards, outputs_per_rank, alpha, bits)
 
     # Value hashes per leaf: the blocks the conversion reads (b = 1 for
     # integers and direct tuples; 2 for Tuple<IntModN32 x 2>: 16 + 4 bytes
@@ -569,9 +613,12 @@ def main():
     bytes_per_launch = outputs_per_rank * esz
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
+    n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    ghz = clock["clock_ghz"]
     if rank == 0:
+        # The committed rocprof summaries are of the one-GPU lines.
         tr = (profiled_traffic(kernel_name(args, bits), outputs_per_rank, workload=workload_tag(args))
-              if args.log_domain == (31 if bits == 128 else LOG_PER_GPU) else None)
+              if shards == 1 and args.log_domain == (31 if bits == 128 else LOG_PER_GPU) else None)
         vname = {"full_domain": "uint64", "full_domain_u128": "uint128",
                  "full_domain_tuple": {"intmodn32x2": "Tuple<IntModN<uint32_t, 4294967291>, "
                                                       "IntModN<uint32_t, 4294967291>>",
@@ -587,34 +634,51 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u32 mod N" if tuple_mod else ("u32" if args.workload == "full_domain_tuple"
                                                    else f"u{bits}"),
             "data": "synthetic: one DpfKey from the product keygen with fixed root seeds",
             "reference_aes_blocks_per_launch": ref_aes_per_launch,
             "config": {"workload": f"full-domain EvaluateUntil(0, {{}}) of one key, "
-                                   f"log_domain_size={log_domain}, {vname}, 2^{args.log_domain} "
-                                   f"outputs per GPU",
+                                   f"log_domain_size={log_domain}, {vname}, "
+                                   f"2^{outputs_per_rank.bit_length() - 1} outputs per GPU",
                        "log_domain_size": log_domain, "value_type": vname,
                        "blocks_needed": dpf.blocks_needed(0), "value_blocks_hashed_per_leaf": b_read,
                        "outputs_per_gpu": outputs_per_rank, "tree_levels_per_gpu": depth,
-                       "parallelism": f"subtree-prefix x{world}"},
+                       "parallelism": f"subtree-prefix x{shards}"},
             "aes_blocks_per_s": aes_per_launch * world * args.steps / elapsed,
             **aes_rooflines(achieved, kernel_name(args, bits),
                             traffic=tr[0] if tr else None,
                             traffic_source=tr[1] if tr else None,
                             pmc=tr[2] if tr else None, launch_ms=kern_ms_max,
                             algorithmic_aes_per_launch=aes_per_launch,
-                            algorithmic_bytes_per_launch=bytes_per_launch),
+                            algorithmic_bytes_per_launch=bytes_per_launch,
+                            sustained_clock_ghz=ghz,
+                            sustained_clock_ghz_per_rank=clocks,
+                            clk_per_aes_per_cu=(kern_ms * 1e-3 * ghz * 1e9 * n_cus / aes_per_launch
+                                                if ghz else None),
+                            clock_source="s_memtime/s_memrealtime stamps of every workgroup of the "
+                                         f"timed launches ({clock['workgroups']} workgroups, "
+                                         f"{clock['mean_workgroup_ms']:.3f} ms each on average)",
+                            cus=n_cus),
+            # Fixed per-step cost: wall time per step beyond the launch's own
+            # HIP-event time (host validation, the packed image, launch gaps).
+            "step_overhead": {"ms_per_step": ms_per_step, "launch_ms": kern_ms_max,
+                              "overhead_ms": ms_per_step - kern_ms_max,
+                              "overhead_frac": (ms_per_step - kern_ms_max) / ms_per_step},
             "process_group": ginfo,
             "roofline_hbm": {"bound": "hbm",
                              "achieved": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9,
                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9 / HBM_PEAK_GBS},
         }
+        if args.rehearse_world:
+            res["rehearsal"] = (f"one process evaluating shard 0 of a {shards}-rank split: "
+                                f"`value` is that shard's rate on one GPU, not an N-GPU result")
         profile_check(res["roofline"], tr, aes_per_launch, kern_ms_max)
-        if args.host_output and world == 1 and args.workload in ("full_domain", "full_domain_u128"):
+        if (args.host_output and world == 1 and shards == 1
+                and args.workload in ("full_domain", "full_domain_u128")):
             res["api_level"] = host_output_rate(dpf, ctx0, bits, args.host_output_reps, out,
                                                 outputs_per_rank, kern_ms_max)
         if world == 1 and not args.no_cpu_baseline:
@@ -624,7 +688,7 @@ def main():
                        if args.tuple_type == "intmodn32x2" else ("tuple", [("int", 32)] * 2))
             res["cpu_baseline"] = cpu_baseline(key, log_domain, args.cpu_chunks, bits, vt=ovt)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if group_up(dist):
         dist.destroy_process_group()
 
 
@@ -767,14 +831,14 @@ def main_evaluate_at(args):
             dpf.evaluate_at_batch_to_device(dbatch, 0, points, ppk, out, stream=stream)
         if evs is not None:
             evs[1].record(stream)
-        if summed and world > 1:
+        if summed and group_up(dist):
             return S.aggregate_shares(dpf, 0, out, ppk)
         return None
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(H.Event(), H.Event()) for _ in range(args.steps)]
@@ -784,7 +848,7 @@ def main_evaluate_at(args):
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     timed_kernel = H.last_points_kernel()   # before the spot checks launch their own
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
@@ -796,7 +860,7 @@ def main_evaluate_at(args):
         s0 = total if total is not None else out.cpu().numpy()
         dpf.evaluate_at_batch_sum_to_device(dpf.upload_key_batch(b1, stream=stream), 0, points,
                                             out, stream=stream)
-        s1 = S.aggregate_shares(dpf, 0, out, ppk) if world > 1 else out.cpu().numpy()
+        s1 = S.aggregate_shares(dpf, 0, out, ppk) if group_up(dist) else out.cpu().numpy()
         rec = (np.asarray(s0).view(np.uint64) + np.asarray(s1).view(np.uint64)).tolist()
         if rec != [1, 1, 1, 1] + [0] * (ppk - 4):
             raise SystemExit(f"rank {rank}: two-server reconstruction failed: {rec[:8]}")
@@ -853,7 +917,7 @@ def main_evaluate_at(args):
                 host_pts = points.view(-1, 2)[:nb * ppk].cpu().numpy().view(np.uint64)
             res["cpu_baseline"] = cpu_baseline_points(dpf, b0, host_pts, nk, ppk)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if group_up(dist):
         dist.destroy_process_group()
 
 
@@ -956,7 +1020,8 @@ def main_heavy_hitters(args):
     max_out = max(4 * args.top_k, 1 << logs[0])
     servers = [HH.Server(dpf, dpf.upload_key_batch(b, stream=stream), max_out, dev)
                for b in (b0, b1)]
-    aggregate = (lambda h, part, n: S.aggregate_shares(dpf, h, part, n)) if world > 1 else None
+    aggregate = ((lambda h, part, n: S.aggregate_shares(dpf, h, part, n)) if group_up(dist)
+                 else None)
     evs = []
 
     class Timed:  # brackets every batched evaluation with hipEvents on `stream`
@@ -980,7 +1045,7 @@ def main_heavy_hitters(args):
     for _ in range(args.warmup):
         one_pass()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs.clear()
@@ -990,7 +1055,7 @@ def main_heavy_hitters(args):
         final = one_pass(record if i == args.steps - 1 else None)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     kern_ms = sum(a.elapsed_ms(b) for a, b in evs) / args.steps
     cache_bytes = [int(srv.ctx.device_bytes) for srv in servers]
@@ -1050,7 +1115,7 @@ def main_heavy_hitters(args):
             res["cpu_baseline"] = cpu_baseline_heavy_hitters(logs, record, alphas, seeds,
                                                              args.top_k)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if group_up(dist):
         dist.destroy_process_group()
 
 
@@ -1109,7 +1174,7 @@ def main_dcf(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(H.Event(), H.Event()) for _ in range(args.steps)]
@@ -1118,7 +1183,7 @@ def main_dcf(args):
         step(evs[i])
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
-    if world > 1:
+    if group_up(dist):
         dist.barrier()
     kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
@@ -1176,7 +1241,7 @@ def main_dcf(args):
                           f"per level, h:83-105) on the oracle (keygen included), {dt:.1f} s "
                           f"wall on {CPU_THREADS} host threads"}
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if group_up(dist):
         dist.destroy_process_group()
 
 

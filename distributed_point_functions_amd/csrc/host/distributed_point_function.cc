@@ -905,7 +905,8 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
   const dpf_block path = ToBlock(static_cast<uint128>(shard));
   std::vector<dpf_block> vcw_blocks(vcw.size());
   for (size_t i = 0; i < vcw.size(); ++i) vcw_blocks[i] = ToBlock(vcw[i]);
-  PackedUploads& up = s->packed;
+  PackedUploads& up = s->shard_alt ? s->packed_alt : s->packed;
+  s->shard_alt = !s->shard_alt;
   DPF_RETURN_IF_ERROR(up.Reset());
   const size_t o_seed = up.Add(&root, 1), o_ctrl = up.Add(&party, 1), o_path = up.Add(&path, 1);
   const size_t o_vcw = up.Add(vcw_blocks.data(), vcw_blocks.size());

@@ -530,7 +530,10 @@ class PackedUploads {
     }
     if (end <= cap_) return;
     void* np = nullptr;
-    const size_t want = std::max<size_t>({end, cap_ + cap_ / 2, size_t{1} << 20});
+    // Grow by half again, never past kMaxPinned (a long-lived
+    // object must not keep ~1.5x the cap page-locked).
+    const size_t want =
+        std::max(end, std::min(std::max<size_t>(cap_ + cap_ / 2, size_t{1} << 20), kMaxPinned));
     if (end > kMaxPinned || dpf_hip_host_alloc(&np, want) != 0) {
       // Too large to keep page-locked (or no page-locked memory): pageable.
       GrowPageable(end, static_cast<const char*>(pinned_));
@@ -651,6 +654,12 @@ class DeviceScratch {
   std::recursive_mutex mu;
   PackedUploads packed;
   PackedUploads packed_pe;   // ComputePartialEvaluations' walk (its seeds feed the expansion)
+  // EvaluateShardToDevice alternates between `packed` and this image, so a
+  // call waits (PackedUploads::Reset) for the launch two calls back, not for
+  // the one still running: back-to-back shard calls keep the GPU busy while
+  // the host builds the next call's image.
+  PackedUploads packed_alt;
+  bool shard_alt = false;
   // EvaluateUntil's prefix dedup, kept across calls so a call of the same
   // size value-initialises nothing.
   std::vector<uint128> tree_indices;

@@ -245,6 +245,41 @@ struct ExpandParams {
   const uint8_t* cw_right;
   char* out;
   RoundKeys rkl, rkr, rkv, rkd;
+  // Clock probe (dpf_hip_clock_probe): NULL, or [shader clocks, 100 MHz ticks,
+  // workgroups] that wave 0 of every workgroup adds its s_memtime /
+  // s_memrealtime deltas around its work into.  Nothing reads it back in the
+  // kernel; no output depends on it.
+  unsigned long long* clock;
+};
+
+// Stamps of the clock probe: wave-uniform (wave 0 of the workgroup), two
+// reads per workgroup, so the probe costs nothing measurable in a launch of
+// milliseconds (MI355X_MICROARCH.md: in-kernel clock = delta s_memtime /
+// delta s_memrealtime x 100 MHz).
+#ifndef DPF_CLOCK_PROBE
+#define DPF_CLOCK_PROBE 1   // 0: stamps compiled out (A/B variant builds)
+#endif
+struct ClockStamp {
+  unsigned long long c0 = 0, r0 = 0;
+  __device__ __forceinline__ void begin(const unsigned long long* acc) {
+    if (DPF_CLOCK_PROBE && acc != nullptr && threadIdx.x < 64) {
+      c0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) before the LDS loop
+    }
+  }
+  __device__ __forceinline__ void end(unsigned long long* acc) {
+    if (DPF_CLOCK_PROBE && acc != nullptr && threadIdx.x < 64) {
+      const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+      const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      if (threadIdx.x == 0) {
+        atomicAdd(acc + 0, c1 - c0);
+        atomicAdd(acc + 1, r1 - r0);
+        atomicAdd(acc + 2, 1ull);
+      }
+    }
+  }
 };
 
 __device__ __forceinline__ Block4 load_block(const dpf_block* p) {

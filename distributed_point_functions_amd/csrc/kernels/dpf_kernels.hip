@@ -44,6 +44,9 @@ namespace dpf_rt {
 thread_local std::string g_last_error;
 thread_local const char* g_last_expand = "";
 thread_local int g_last_expand_s = -1;
+// dpf_hip_clock_probe's device accumulator (NULL: off), read by every
+// dpf_hip_expand launch.
+std::atomic<unsigned long long*> g_clock_acc{nullptr};
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -282,6 +285,8 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
   const int k0 = p.k0, S = p.S;
   const int G = S - 3;
   const int64_t ngroups = (int64_t)1 << G;
+  ClockStamp stamp;
+  stamp.begin(p.clock);
   for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
        item += (int64_t)gridDim.x * blockDim.x) {
     // 1. walk from the start seed to this item's subtree root.
@@ -372,6 +377,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
       }
     }
   }
+  stamp.end(p.clock);
 }
 
 // Batched point evaluation (row a11).  Work item u covers
@@ -1182,6 +1188,36 @@ const char* dpf_hip_last_expand_kernel(int* subtree_depth) {
   return dpf_rt::g_last_expand;
 }
 
+int dpf_hip_clock_probe(int on) {
+  unsigned long long* old = dpf_rt::g_clock_acc.exchange(nullptr);
+  if (old) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipFree(old));
+  }
+  if (!on) return kOk;
+  void* p = nullptr;
+  HIP_TRY(hipMalloc(&p, 4 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(p, 0, 4 * sizeof(unsigned long long)));
+  HIP_TRY(hipDeviceSynchronize());
+  dpf_rt::g_clock_acc.store(static_cast<unsigned long long*>(p));
+  return kOk;
+}
+
+int dpf_hip_clock_probe_read(double* clock_ghz, int64_t* workgroups, double* mean_workgroup_s) {
+  unsigned long long* acc = dpf_rt::g_clock_acc.load();
+  if (!acc) return fail(kFailedPrecondition, "clock probe is off (dpf_hip_clock_probe(1))");
+  unsigned long long h[4] = {0, 0, 0, 0};
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h, acc, sizeof(h), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemset(acc, 0, sizeof(h)));
+  HIP_TRY(hipDeviceSynchronize());
+  // s_memtime counts shader clocks, s_memrealtime a constant 100 MHz.
+  if (clock_ghz) *clock_ghz = h[1] ? (double)h[0] / (double)h[1] * 0.1 : 0.0;
+  if (workgroups) *workgroups = (int64_t)h[2];
+  if (mean_workgroup_s) *mean_workgroup_s = h[2] ? (double)h[1] / (double)h[2] * 1e-8 : 0.0;
+  return kOk;
+}
+
 int dpf_hip_device_count(int* count) {
   HIP_TRY(hipGetDeviceCount(count));
   return kOk;
@@ -1932,6 +1968,7 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
   p.rkr = expand_key(key_right);
   p.rkv = expand_key(key_value);
   p.rkd = xor_keys(p.rkl, p.rkr);
+  p.clock = dpf_rt::g_clock_acc.load(std::memory_order_relaxed);
   hipStream_t s = (hipStream_t)stream;
   if (fast_int(desc)) {
     const int bits = desc->bits[0], E = desc->elements_per_block;

@@ -11,8 +11,8 @@
 
 namespace dpf_rt {
 
-constexpr int kOk = 0, kInvalidArgument = 3, kResourceExhausted = 8, kUnimplemented = 12,
-              kInternal = 13;
+constexpr int kOk = 0, kInvalidArgument = 3, kResourceExhausted = 8, kFailedPrecondition = 9,
+              kUnimplemented = 12, kInternal = 13;
 
 // Records `msg` as the calling thread's last error and returns `code`.
 int fail(int code, const std::string& msg);

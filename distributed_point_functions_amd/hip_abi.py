@@ -93,6 +93,10 @@ def load(require_gpu: bool = False):
         L.dpf_hip_event_record.argtypes = [P, P]
         L.dpf_hip_event_elapsed_ms.argtypes = [P, P, ctypes.POINTER(ctypes.c_float)]
         L.dpf_hip_stream_sync.argtypes = [P]
+        L.dpf_hip_clock_probe.argtypes = [I]
+        L.dpf_hip_clock_probe_read.argtypes = [ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_int64),
+                                               ctypes.POINTER(ctypes.c_double)]
         _lib = L
     if require_gpu:
         import torch
@@ -119,6 +123,19 @@ def last_points_kernel() -> str:
     """Kernel of this thread's last point evaluation, e.g. "points/ilp4" --
     dispatch diagnostics for the tests."""
     return load().dpf_hip_last_points_kernel().decode()
+
+
+def clock_probe(on: bool) -> None:
+    """Turns the expand launches' in-kernel clock probe on (zeroed) or off."""
+    check(load(require_gpu=True).dpf_hip_clock_probe(1 if on else 0))
+
+
+def clock_probe_read() -> dict:
+    """Sustained shader clock (GHz) of the octet expand launches since the
+    last read, from s_memtime / s_memrealtime stamps of every workgroup."""
+    ghz, wg, mean_s = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+    check(load().dpf_hip_clock_probe_read(ctypes.byref(ghz), ctypes.byref(wg), ctypes.byref(mean_s)))
+    return {"clock_ghz": ghz.value, "workgroups": wg.value, "mean_workgroup_ms": mean_s.value * 1e3}
 
 
 def check(st: int):

@@ -11,7 +11,10 @@ covers output elements [r * n / N, (r + 1) * n / N): concatenating the shards
 in rank order is the reference's full-domain output.  There is no exchange on
 the data path; the only collective is the max-over-ranks of the step time.
 
-Weak scaling (bench.py): every rank keeps 2^log_per_gpu outputs, so the
+Strong scaling (bench.py's default, the metric's configuration: one 2^30
+domain at 1/2/4/8 GPUs): the domain stays 2^log_domain and each rank
+evaluates 2^(log_domain - k) outputs.  Weak scaling (`--scaling weak`, and
+config 3's uint128 default): every rank keeps 2^log_per_gpu outputs, so the
 domain grows to 2^(log_per_gpu + k) with N.
 """
 from __future__ import annotations
@@ -29,6 +32,14 @@ def weak_scaling_log_domain(log_per_gpu: int, world: int) -> int:
     return log_per_gpu + shard_bits(world)
 
 
+def strong_scaling_log_outputs(log_domain: int, world: int) -> int:
+    """log2 of the outputs each of `world` ranks evaluates of one 2^log_domain domain."""
+    k = shard_bits(world)
+    if k > log_domain:
+        raise ValueError(f"{world} shards of a 2^{log_domain} domain")
+    return log_domain - k
+
+
 def shard_range(num_outputs: int, world: int, rank: int) -> tuple:
     """[start, stop) of the output elements rank `rank` produces."""
     shard_bits(world)
@@ -42,10 +53,11 @@ def shard_range(num_outputs: int, world: int, rank: int) -> tuple:
 
 def max_over_ranks(value: float, device=None) -> float:
     """Max of a per-rank scalar (the step time) over the process group; the
-    identity without an initialised group."""
+    identity without an initialised group (a one-rank group still runs the
+    collective, so the RCCL path is exercised on a one-GPU box)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64,
                      device=device if device is not None else "cpu")
@@ -58,7 +70,7 @@ def gather_over_ranks(value: float, device=None) -> list:
     an initialised group)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [float(value)]
     t = torch.tensor([float(value)], dtype=torch.float64,
                      device=device if device is not None else "cpu")
@@ -108,7 +120,7 @@ def all_gather_shares(packed):
     import numpy as np
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return packed.cpu().numpy().reshape(1, -1)
     if packed.is_cuda and dist.get_backend() == "gloo":
         packed = packed.cpu()   # gloo all-gathers host tensors only
@@ -180,8 +192,7 @@ def aggregate_shares(dpf, hierarchy_level: int, packed, count: int):
     import torch.distributed as dist
     from . import dpf as D
     leaves = D.leaves_of(dpf.parameters()[hierarchy_level].value_type)
-    if (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-            and _widenable(leaves)):
+    if dist.is_available() and dist.is_initialized() and _widenable(leaves):
         return all_reduce_shares(leaves, packed, count)
     stacked = all_gather_shares(packed)
     return dpf.sum_packed_shares(hierarchy_level, stacked, stacked.shape[0], count)

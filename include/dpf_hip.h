@@ -191,6 +191,20 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
  * chose.  Tests use it to pin the dispatch. */
 const char* dpf_hip_last_expand_kernel(int* subtree_depth);
 
+/* Diagnostic (bench.py): the sustained shader clock of the expand launches
+ * themselves.  dpf_hip_clock_probe(1) allocates and zeroes a device
+ * accumulator on the current device; from then on wave 0 of every
+ * workgroup of every octet expand launch (the full-domain kernel) adds its
+ * s_memtime (shader clocks) and s_memrealtime (100 MHz) deltas around its
+ * work into it -- two stamps per workgroup, nothing on the outputs' path.
+ * dpf_hip_clock_probe_read waits for the device, returns the clock in GHz
+ * (sum of shader-clock deltas / sum of real-time deltas), the number of
+ * stamped workgroups and their mean duration in seconds, and zeroes the
+ * accumulator.  dpf_hip_clock_probe(0) turns it off.  No reference
+ * counterpart (SURVEY.md 8d asks for the sustained clock). */
+int dpf_hip_clock_probe(int on);
+int dpf_hip_clock_probe_read(double* clock_ghz, int64_t* workgroups, double* mean_workgroup_s);
+
 /* Diagnostic: which kernel the calling thread's last
  * dpf_hip_eval_prefix_batch(_cached) launched: "hh_level" (the lean
  * heavy-hitters kernel: cached or gathered start seeds, two expanded levels,

@@ -97,3 +97,37 @@ def test_launcher_cmd_relaunches_same_arguments(bench):
     assert cmd[cmd.index("--master-port") + 1] == "29511"
     assert cmd[-4:] == ["--gpus", "8", "--steps", "5"]
     assert os.path.basename(cmd[-5]) == "bench.py"
+
+
+def _parse(bench, argv):
+    old = sys.argv
+    sys.argv = ["bench.py", *argv]
+    try:
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+def test_default_line_is_the_metric_configuration(bench):
+    # BASELINE metric: ONE 2^30 uint64 domain at 1/2/4/8 GPUs -> strong
+    # scaling by default; the drop-in API rate (api_level) on by default.
+    a = _parse(bench, [])
+    assert a.workload == "full_domain" and a.log_domain == 30
+    assert a.scaling == "strong" and a.host_output
+    assert _parse(bench, ["--gpus", "8"]).scaling == "strong"
+    assert not _parse(bench, ["--no-host-output"]).host_output
+    assert _parse(bench, ["--scaling", "weak"]).scaling == "weak"
+    # config 3 (2^34 uint128 over 8 GPUs = 2^31 per GPU): weak by default.
+    assert _parse(bench, ["--workload", "full_domain_u128"]).scaling == "weak"
+    with pytest.raises(SystemExit):
+        _parse(bench, ["--gpus", "2", "--rehearse-world", "8"])
+    assert _parse(bench, ["--rehearse-world", "8"]).rehearse_world == 8
+
+
+def test_line_keys_pinned_in_source(bench):
+    # The keys the driver's line carries beside `value` (bench.py builds them
+    # only on a GPU; pinned here by source so a refactor cannot drop them).
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    for key in ('"scaling": args.scaling', "sustained_clock_ghz=", "clk_per_aes_per_cu=",
+                '"step_overhead"', 'res["api_level"]', "H.clock_probe(True)"):
+        assert key in src, key

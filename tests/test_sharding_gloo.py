@@ -36,13 +36,19 @@ def _shard_with_oracle(P, key, h, world, rank):
                           O._value_correction(P, key, h), key["party"])
 
 
-def _worker(rank, world, port, log_per_gpu, q):
+def _log_domain(scaling, log, world):
+    """bench.py's domain: fixed (strong, the metric's configuration) or grown
+    with the world (weak)."""
+    return log if scaling == "strong" else S.weak_scaling_log_domain(log, world)
+
+
+def _worker(rank, world, port, scaling, log, q):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        log_domain = S.weak_scaling_log_domain(log_per_gpu, world)
+        log_domain = _log_domain(scaling, log, world)
         P = O.OracleParams([(log_domain, ("int", 64), 0)])
         k0, k1 = O.generate_keys(P, 0x1234567 % (1 << log_domain), [[42]], 5, 6)
         res = {}
@@ -59,13 +65,16 @@ def _worker(rank, world, port, log_per_gpu, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_shards_concatenate_to_full_domain(world):
-    log_per_gpu = 10
+@pytest.mark.parametrize("world,scaling", [(2, "strong"), (4, "strong"), (8, "strong"),
+                                           (2, "weak"), (4, "weak")])
+def test_shards_concatenate_to_full_domain(world, scaling):
+    # strong: one 2^12 domain split `world` ways (bench.py's default, the
+    # metric's fixed-domain configuration); weak: 2^10 outputs per rank.
+    log = 12 if scaling == "strong" else 10
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, log_per_gpu, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, scaling, log, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -74,22 +83,30 @@ def test_shards_concatenate_to_full_domain(world):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert t == world - 0.5
-    log_domain = S.weak_scaling_log_domain(log_per_gpu, world)
+    log_domain = _log_domain(scaling, log, world)
+    per_rank = S.strong_scaling_log_outputs(log_domain, world)
+    if scaling == "weak":
+        assert per_rank == log
     P = O.OracleParams([(log_domain, ("int", 64), 0)])
     k0, k1 = O.generate_keys(P, 0x1234567 % (1 << log_domain), [[42]], 5, 6)
     for key in (k0, k1):
         full = O.evaluate_until(P, 0, [], O.create_context(P, key))
         parts = res[key["party"]]
         n = len(full)
+        assert n == 1 << log_domain
         for r, part in enumerate(parts):
             a, b = S.shard_range(n, world, r)
-            assert part.shape[0] == b - a == 1 << log_per_gpu
+            assert part.shape[0] == b - a == 1 << per_rank
         np.testing.assert_array_equal(np.concatenate(parts), full)
 
 
 def test_partition_helpers():
     assert S.shard_bits(1) == 0 and S.shard_bits(8) == 3
     assert S.weak_scaling_log_domain(30, 8) == 33
+    assert S.strong_scaling_log_outputs(30, 8) == 27
+    assert S.strong_scaling_log_outputs(30, 1) == 30
+    with pytest.raises(ValueError):
+        S.strong_scaling_log_outputs(2, 8)
     assert S.shard_range(16, 4, 3) == (12, 16)
     for bad in (0, 3, 6):
         with pytest.raises(ValueError):
