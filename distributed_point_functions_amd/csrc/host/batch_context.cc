@@ -228,7 +228,12 @@ StatusOr<std::unique_ptr<DeviceBatchContext>> DistributedPointFunction::CreateBa
   if (keys.num_levels() != tree_levels_needed() - 1 ||
       keys.num_hierarchy_levels() != static_cast<int>(parameters().size()))
     return InvalidArgumentError("key batch does not match this DistributedPointFunction");
-  return std::unique_ptr<DeviceBatchContext>(new DeviceBatchContext(&keys));
+  std::unique_ptr<DeviceBatchContext> ctx(new DeviceBatchContext(&keys));
+  // DPF_BATCH_KEY_MAJOR=1 (read at creation: one layout per context) keeps
+  // the r15 key-major tables and lanes = start nodes (A/B and test hook).
+  const char* km = std::getenv("DPF_BATCH_KEY_MAJOR");
+  ctx->index_major_ = !(km && km[0] == '1');
+  return ctx;
 }
 
 StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchToDevice(
@@ -552,10 +557,10 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     DPF_RETURN_IF_ERROR(ensure(&ctx.slots_, &ctx.slots_cap_, T * sizeof(int64_t)));
     HIP_RETURN_IF_ERROR(
         dpf_hip_memcpy_h2d(ctx.slots_, start_slot.data(), T * sizeof(int64_t), stream));
-    HIP_RETURN_IF_ERROR(dpf_hip_gather_seeds(
+    HIP_RETURN_IF_ERROR(dpf_hip_gather_seeds_layout(
         K, T, static_cast<const int64_t*>(ctx.slots_), static_cast<const dpf_block*>(ctx.leaf_seeds_),
         ctx.leaf_stride_, static_cast<dpf_block*>(ctx.next_seeds_),
-        static_cast<uint8_t*>(ctx.next_ctrl_), stream));
+        static_cast<uint8_t*>(ctx.next_ctrl_), ctx.index_major_ ? 1 : 0, stream));
     cache_in_use = false;  // copied out; from here on only the write target
     ctx.leaf_level_ = -1;  // rewritten in place by this call's kernel
     const size_t cache_need = static_cast<size_t>(K * leaf_stride) * sizeof(dpf_block);
@@ -598,7 +603,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
                                : gather ? T
                                         : static_cast<int64_t>(ctx.partial_prefixes_.size());
   auto launch = [&](int sum_mode, void* out, uint64_t* workspace) {
-    return FromHip(dpf_hip_eval_prefix_batch_cached_slots(
+    return FromHip(dpf_hip_eval_prefix_batch_layout(
         K, U, Wk + s, update_ctx && !gather ? Wk : -1, E, cached ? Dprev : start_level,
         keys.num_levels(), keys.seed(), keys.party(), start_seeds, start_ctrl, start_stride,
         static_cast<const int32_t*>(ctx.parent_), static_cast<const dpf_block*>(ctx.path_),
@@ -606,7 +611,8 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         static_cast<uint8_t*>(ctx.next_ctrl_), T, keys.cw_seed(), keys.cw_left(), keys.cw_right(),
         &kl, &kr, &kv, &desc, cepb, keys.value_correction(hierarchy_level), sum_mode, workspace,
         out, static_cast<dpf_block*>(leaf_seeds), cache_stride,
-        permute ? static_cast<const int32_t*>(ctx.leaf_slot_) : nullptr, stream));
+        permute ? static_cast<const int32_t*>(ctx.leaf_slot_) : nullptr, ctx.index_major_ ? 1 : 0,
+        stream));
   };
   if (native_sum) {
     void* target = device_out;
@@ -700,9 +706,19 @@ StatusOr<EvaluationContext> DistributedPointFunction::ExportEvaluationContext(
     const int64_t Q = static_cast<int64_t>(q.size());
     std::vector<dpf_block> seeds(Q);
     std::vector<uint8_t> ctrl(Q);
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds.data(), ctx.partial_seeds() + k * Q,
-                                           Q * sizeof(dpf_block), stream));
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(ctrl.data(), ctx.partial_control() + k * Q, Q, stream));
+    if (ctx.index_major()) {
+      // Key k's column of the [prefix][key] tables.
+      const int64_t K = keys.num_keys();
+      HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h_strided(seeds.data(), ctx.partial_seeds() + k,
+                                                     sizeof(dpf_block), K * sizeof(dpf_block), Q,
+                                                     stream));
+      HIP_RETURN_IF_ERROR(
+          dpf_hip_memcpy_d2h_strided(ctrl.data(), ctx.partial_control() + k, 1, K, Q, stream));
+    } else {
+      HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(seeds.data(), ctx.partial_seeds() + k * Q,
+                                             Q * sizeof(dpf_block), stream));
+      HIP_RETURN_IF_ERROR(dpf_hip_memcpy_d2h(ctrl.data(), ctx.partial_control() + k * Q, Q, stream));
+    }
     for (int64_t i = 0; i < Q; ++i) {
       PartialEvaluation* e = out.add_partial_evaluations();
       SetProtoBlock(q[i], e->mutable_prefix());

@@ -89,8 +89,18 @@ struct BatchLevelParams {
   dpf_block* leaf_seeds;
   int64_t leaf_stride;
   const int32_t* leaf_slot;   // NULL: leaf l of start node u at slot (u << E) + l
+  // Layout of seeds_in / ctrl_in, seeds_out / ctrl_out and leaf_seeds:
+  // 0 = key-major (element (k, j) at k * stride + j), 1 = index-major (at
+  // j * num_keys + k, the device batch context's layout).
+  int index_major;
   RoundKeys rkl, rkr, rkd, rkv;
 };
+
+// Element (key k, slot j) of a per-key table with `stride` slots per key.
+__device__ __forceinline__ int64_t tab_at(const BatchLevelParams& p, int64_t k, int64_t j,
+                                          int64_t stride) {
+  return p.index_major ? j * p.num_keys + k : k * stride + j;
+}
 
 __device__ __forceinline__ uint4 cw_block(const dpf_block* p) {
   const dpf_block c = *p;
@@ -365,7 +375,7 @@ struct GenericV {
 template <int MAXE, class V, class Sink>
 __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const BatchLevelParams& p,
                                                    const V& v, int64_t k, Block4 node,
-                                                   uint32_t t, int64_t leaf_row,
+                                                   uint32_t t, bool store_leaves,
                                                    int64_t leaf_first, Sink&& sink) {
   Block4 N[1 << MAXE];
   uint32_t T = 0;  // bit i = control bit of N[i]
@@ -410,14 +420,14 @@ __device__ __forceinline__ void expand_and_convert(const LdsLookup& lk, const Ba
   // 2^E consecutive entries per lane.
   // With a slot table (the cache rewritten in place, permuted) leaf i goes
   // to its own slot; this thread has already read every cache entry it reads.
-  if (leaf_row >= 0) {
+  if (store_leaves) {
 #pragma unroll
     for (int i = 0; i < (1 << MAXE); ++i) {
       if (i < (1 << E)) {
         Block4 c = N[i];
         c.w0 |= (T >> i) & 1u;
         const int64_t slot = p.leaf_slot ? p.leaf_slot[leaf_first + i] : leaf_first + i;
-        store_block(p.leaf_seeds + leaf_row + slot, c);
+        store_block(p.leaf_seeds + tab_at(p, k, slot, p.leaf_stride), c);
       }
     }
   }
@@ -470,11 +480,12 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
       Block4 sa, sb;
       uint32_t ta, tb;
       if (p.seeds_in) {
-        sa = load_block(p.seeds_in + ka * p.in_stride + par);
-        sb = load_block(p.seeds_in + kb * p.in_stride + par);
+        const int64_t ia = tab_at(p, ka, par, p.in_stride), ib = tab_at(p, kb, par, p.in_stride);
+        sa = load_block(p.seeds_in + ia);
+        sb = load_block(p.seeds_in + ib);
         if (p.ctrl_in) {
-          ta = p.ctrl_in[ka * p.in_stride + par] & 1u;
-          tb = p.ctrl_in[kb * p.in_stride + par] & 1u;
+          ta = p.ctrl_in[ia] & 1u;
+          tb = p.ctrl_in[ib] & 1u;
         } else {
           // Expansion cache layout: the control bit rides in bit 0 of the seed.
           ta = sa.w0 & 1u;
@@ -498,11 +509,13 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
       const uint8_t* rb = p.cw_right + kb * p.cw_stride + p.cw_first;
       for (int j = 0; j <= W; ++j) {
         if (j == p.save_after && save >= 0 && valid) {
-          store_block(p.seeds_out + ka * p.out_stride + save, sa);
-          p.ctrl_out[ka * p.out_stride + save] = (uint8_t)ta;
+          const int64_t oa = tab_at(p, ka, save, p.out_stride);
+          store_block(p.seeds_out + oa, sa);
+          p.ctrl_out[oa] = (uint8_t)ta;
           if (has_b) {
-            store_block(p.seeds_out + kb * p.out_stride + save, sb);
-            p.ctrl_out[kb * p.out_stride + save] = (uint8_t)tb;
+            const int64_t ob = tab_at(p, kb, save, p.out_stride);
+            store_block(p.seeds_out + ob, sb);
+            p.ctrl_out[ob] = (uint8_t)tb;
           }
         }
         if (j == W) break;
@@ -520,10 +533,10 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
         vk.key(p, k);
         const Block4 node = which ? sb : sa;
         const uint32_t tn = which ? tb : ta;
-        const int64_t leaf_row = p.leaf_seeds && valid ? k * p.leaf_stride : -1;
+        const bool store_leaves = p.leaf_seeds && valid;
         const int64_t leaf_first = u << p.expand_levels;
         if constexpr (SUM) {
-          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_row, leaf_first,
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, store_leaves, leaf_first,
                                    [&](int l, const typename V::Val& val) {
 #pragma unroll
             for (int i = 0; i < (1 << MAXE); ++i)
@@ -531,7 +544,7 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
           });
         } else {
           char* row = p.out + k * p.out_row + (u << p.expand_levels) * (int64_t)p.epl * p.esz;
-          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, leaf_row, leaf_first,
+          expand_and_convert<MAXE>(lk, p, vk, k, node, tn, store_leaves, leaf_first,
                                    [&](int l, const typename V::Val& val) {
             if (valid) vk.store(lk, p, row + (int64_t)l * p.epl * p.esz, val);
           });
@@ -581,7 +594,8 @@ __global__ void sum_rows_kernel(int64_t rows, int64_t row_len, dpf_value_desc d,
 }
 
 // Start seeds of a call from the previous call's expansion cache:
-// seeds_out[k*T + i] = cache[k*cache_stride + slot[i]] (and the control bits).
+// seeds_out[k*T + i] = cache[k*cache_stride + slot[i]] (and the control bits);
+// index_major: seeds_out[i*keys + k] = cache[slot[i]*keys + k].
 __global__ void gather_seeds_kernel(int64_t keys, int64_t T, const int64_t* __restrict__ slot,
                                     const dpf_block* __restrict__ cache, int64_t cache_stride,
                                     dpf_block* __restrict__ seeds_out,
@@ -610,6 +624,24 @@ __global__ void gather_seeds_kernel(int64_t keys, int64_t T, const int64_t* __re
         }
       }
     }
+  }
+}
+
+// Index-major form of gather_seeds_kernel: thread = one (row i, key k) pair
+// with k fastest, so a wave reads one 1 KiB run of cache row slot[i] and
+// writes one 1 KiB run of output row i.
+__global__ void gather_seeds_im_kernel(int64_t keys, int64_t T, const int64_t* __restrict__ slot,
+                                       const dpf_block* __restrict__ cache,
+                                       dpf_block* __restrict__ seeds_out,
+                                       uint8_t* __restrict__ ctrl_out) {
+  const int64_t total = keys * T;
+  for (int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = x / keys, k = x - i * keys;
+    Block4 c = load_block(cache + slot[i] * keys + k);
+    ctrl_out[x] = (uint8_t)(c.w0 & 1u);
+    c.w0 &= ~1u;
+    store_block(seeds_out + x, c);
   }
 }
 
@@ -694,10 +726,25 @@ int dpf_hip_eval_prefix_batch(int64_t num_keys, int64_t num_starts, int walk_lev
 int dpf_hip_gather_seeds(int64_t num_keys, int64_t num_rows, const int64_t* slot,
                          const dpf_block* cache, int64_t cache_stride, dpf_block* seeds_out,
                          uint8_t* control_out, void* stream) {
+  return dpf_hip_gather_seeds_layout(num_keys, num_rows, slot, cache, cache_stride, seeds_out,
+                                     control_out, 0, stream);
+}
+
+int dpf_hip_gather_seeds_layout(int64_t num_keys, int64_t num_rows, const int64_t* slot,
+                                const dpf_block* cache, int64_t cache_stride, dpf_block* seeds_out,
+                                uint8_t* control_out, int index_major, void* stream) {
   if (num_keys < 0 || num_rows < 0 || cache_stride < 0) return fail(kInvalidArgument, "bad sizes");
   const int64_t total = num_keys * num_rows;
   if (total == 0) return kOk;
   if (!slot || !cache || !seeds_out || !control_out) return fail(kInvalidArgument, "NULL pointer");
+  if (index_major) {
+    int64_t g = (total + 255) / 256;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL(gather_seeds_im_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream,
+                       num_keys, num_rows, slot, cache, seeds_out, control_out);
+    HIP_TRY(hipGetLastError());
+    return kOk;
+  }
   int64_t gx = (num_rows + 255) / 256;
   if (gx > 64) gx = 64;
   // DPF_BATCH_GATHER_KEYS=1|2|4 (read per call; default 4): keys per lane and
@@ -742,6 +789,25 @@ int dpf_hip_eval_prefix_batch_cached_slots(
     const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
     const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
     dpf_block* leaf_cache, int64_t leaf_stride, const int32_t* leaf_slot, void* stream) {
+  return dpf_hip_eval_prefix_batch_layout(
+      num_keys, num_starts, walk_levels, save_after, expand_levels, cw_first, cw_stride, key_seed,
+      party, seeds_in, control_in, in_stride, parent, path, save_index, seeds_out, control_out,
+      out_stride, cw_seed, cw_left, cw_right, key_left, key_right, key_value, desc,
+      elements_per_leaf, value_correction, sum, workspace, out, leaf_cache, leaf_stride, leaf_slot,
+      0, stream);
+}
+
+int dpf_hip_eval_prefix_batch_layout(
+    int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
+    int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
+    const dpf_block* seeds_in, const uint8_t* control_in, int64_t in_stride,
+    const int32_t* parent, const dpf_block* path, const int32_t* save_index, dpf_block* seeds_out,
+    uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed, const uint8_t* cw_left,
+    const uint8_t* cw_right, const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+    const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
+    const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
+    dpf_block* leaf_cache, int64_t leaf_stride, const int32_t* leaf_slot, int index_major,
+    void* stream) {
   int st = validate_desc(desc);
   if (st) return st;
   const int max_e = dpf_hip_prefix_batch_max_expand(desc, sum);
@@ -757,6 +823,7 @@ int dpf_hip_eval_prefix_batch_cached_slots(
   hipStream_t s = (hipStream_t)stream;
   const int64_t slots = (num_starts << expand_levels) * elements_per_leaf;
   const int nl = desc->num_leaves;
+  int sum_words = 3;   // hh_keys_kernel (index-major) sums into one uint64 per element
   if (sum) {
     if (!workspace || !out) return fail(kInvalidArgument, "NULL pointer");
     HIP_TRY(hipMemsetAsync(workspace, 0, (size_t)slots * nl * 3 * sizeof(uint64_t), s));
@@ -807,6 +874,7 @@ int dpf_hip_eval_prefix_batch_cached_slots(
     p.out_row = slots * p.esz;
     p.out = (char*)out;
     p.wide = reinterpret_cast<unsigned long long*>(workspace);
+    p.index_major = index_major ? 1 : 0;
     if (leaf_cache) {
       if (leaf_stride < (num_starts << expand_levels))
         return fail(kInvalidArgument, "expansion cache too small");
@@ -861,12 +929,14 @@ int dpf_hip_eval_prefix_batch_cached_slots(
       a.leaf_slot = p.leaf_slot;
       a.nl = nl;
       a.b = b;
+      a.index_major = p.index_major;
       for (int k = 0; k < nl; ++k) a.mod[k] = (uint32_t)desc->mod_low[k];
       a.key_left = key_left;
       a.key_right = key_right;
       a.key_value = key_value;
       st = launch_hh_level(a, s);
-      g_last_batch_kernel = "hh_level";
+      if (a.index_major) sum_words = 1;
+      g_last_batch_kernel = a.index_major ? "hh_keys" : "hh_level";
     } else if (fast_int(desc)) {
       g_last_batch_kernel = "batch_level/fast";
       const int xm = desc->kind[0] == DPF_LEAF_XOR;
@@ -893,7 +963,8 @@ int dpf_hip_eval_prefix_batch_cached_slots(
     int64_t g = (slots + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(finalize_sums_kernel, dim3((unsigned)g), dim3(256), 0, s, slots, *desc,
-                       reinterpret_cast<const unsigned long long*>(workspace), (char*)out);
+                       reinterpret_cast<const unsigned long long*>(workspace), (char*)out,
+                       sum_words);
     HIP_TRY(hipGetLastError());
   }
   return kOk;

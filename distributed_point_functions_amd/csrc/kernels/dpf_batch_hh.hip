@@ -107,6 +107,21 @@ __device__ __forceinline__ void sample2(const HHParams& p, const Div32 (&div)[2]
   }
 }
 
+// sample2 with the divisors passed directly (hh_keys_kernel).
+__device__ __forceinline__ void sample2_nl(int nl, const Div32& d0, const Div32& d1,
+                                           const Block4& h0, uint32_t w4, uint32_t out[2]) {
+  const uint32_t blk[4] = {h0.w0, h0.w1, h0.w2, h0.w3};
+  uint32_t q[3];
+  out[0] = divmod128(blk, d0, q);
+  if (nl > 1) {
+    const uint32_t nb[4] = {w4, q[0], q[1], q[2]};
+    uint32_t q2[3];
+    out[1] = divmod128(nb, d1, q2);
+  } else {
+    out[1] = 0;
+  }
+}
+
 // DPF_HH_PIN_DIV=1: wave-uniform kernel arguments copied into SGPRs by an
 // instruction the compiler cannot rematerialise, so under SGPR pressure it
 // spills the copy to a VGPR lane (v_writelane / v_readlane, no wait) instead
@@ -339,13 +354,395 @@ void hh_level_kernel(HHParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// hh_keys_kernel: the same level with LANES = KEYS (r16, the default).
+//
+// The device batch context keeps its per-key tables index-major -- the
+// expansion cache, the partial evaluations and the gathered start seeds hold
+// element (key k, slot j) at j * K + k -- so one wave = 64 consecutive keys at
+// ONE (wave-uniform) start node u reads its start seeds as one 1 KiB access
+// and writes each of its four cache leaves and its partial evaluation as one
+// 1 KiB access, whatever slots the level selected.  (hh_level_kernel, lanes =
+// start nodes of one key, read 16-byte entries scattered across a 64 KiB
+// key-major cache row: 4.1x read amplification, waves waiting 20% of their
+// life)  The key's correction words, value correction and party
+// are loaded once per wave into VGPRs and serve every start node; the wave's
+// 64 keys' values of the node's 4 leaves x nl elements are summed mod N
+// across the lanes by a transpose-reduction (10 lane exchanges for 8 sums)
+// and added with ONE atomic instruction of 8 lanes into 64 contiguous bytes
+// of uint64 sums (sums of < N < 2^32 values over <= 2^31 keys fit), reduced
+// mod N by finalize_sums_kernel (words = 1).  Waves start their start-node
+// loop at different nodes so the atomics of resident waves spread over the
+// level's nodes.
+struct HHKeysParams {
+  int64_t num_keys;     // K
+  int64_t num_starts;   // U
+  int64_t u_ranges;     // start-node ranges per 64-key group
+  int64_t u_per_range;
+  int64_t num_waves;    // ceil(K / 64) * u_ranges
+  int cw_level;
+  int cw_stride;
+  int nl;
+  int b;
+  const dpf_block* seeds_in;   // [j][K]
+  const uint8_t* ctrl_in;      // [j][K]; NULL: control bit in bit 0 of the seed
+  const int32_t* parent;
+  const int32_t* save_index;   // NULL: no partial evaluations stored
+  dpf_block* seeds_out;        // [save][K]
+  uint8_t* ctrl_out;
+  const dpf_block* cw_seed;    // [k][cw_stride] (the key batch's own layout)
+  const uint8_t* cw_left;
+  const uint8_t* cw_right;
+  const dpf_block* vcw;
+  int vcw_stride;
+  const uint8_t* party;
+  const uint4* key_tab;        // DPF_HH_KEYS_MODE 2: [3][K], hh_key_table_kernel
+  unsigned long long* sums;    // [(u << 2 | leaf) * nl + e]
+  dpf_block* leaf_seeds;       // [slot][K]; NULL: no expansion cache written
+  const int32_t* leaf_slot;    // NULL: leaf i of start node u at slot (u << 2) + i
+  Div32 div[2];
+  RoundKeys rkl, rkr, rkv;
+};
+
+// Sum over the wave's 64 lanes of eight u32 values v[i] (element i & 1: mod
+// n0 or n1), in VALU lane permutes (no LDS, no address registers): three
+// halving exchanges -- lanes ^ 32 (v_permlane32_swap), ^ 16
+// (v_permlane16_swap), ^ 8 (DPP row_ror:8) -- after which lane L holds a
+// partial sum of value L >> 3, completed over lanes ^ 4 (ds_swizzle), ^ 2 and
+// ^ 1 (DPP quad_perm).  Lanes 8i return the sum of value i.  A slot's value
+// index keeps the parity of the slot, so slot parity picks the modulus.
+__device__ __forceinline__ uint32_t wave_sum8_mod(uint32_t v[8], uint32_t n0, uint32_t n1) {
+  // The swaps exchange vdst's upper half (rows) with vsrc's lower: per lane
+  // the two results are its own kept value and its partner's matching one.
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v[i], v[4 + i], false, false);
+    v[i] = mod_add(r[0], r[1], (i & 1) ? n1 : n0);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v[i], v[2 + i], false, false);
+    v[i] = mod_add(r[0], r[1], (i & 1) ? n1 : n0);
+  }
+  const bool hi8 = (threadIdx.x & 8) != 0;
+  const uint32_t n = hi8 ? n1 : n0;
+  const uint32_t keep = hi8 ? v[1] : v[0], give = hi8 ? v[0] : v[1];
+  uint32_t x = mod_add(keep, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)give, 0x128, 0xF, 0xF, false), n);
+  x = mod_add(x, (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x101F), n);        // lane ^ 4
+  x = mod_add(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false), n);  // ^ 2
+  x = mod_add(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false), n);  // ^ 1
+  return x;
+}
+
+// Where hh_keys_kernel gets each key's two levels of correction words, its
+// value correction and its party (DPF_HH_KEYS_MODE):
+//   2 (default): a per-call key table built by hh_key_table_kernel, [3][K]
+//     uint4 (cs0, cs1, {cc bits | party << 4, corr0, corr1}), re-read for
+//     every start node next to its use as three coalesced 1 KiB loads per
+//     wave (L2 hits), at 4 waves per SIMD;
+//   1: loaded ONCE per wave into 11 VGPRs (135 VGPRs: 3 waves per SIMD):
+//     22.8 vs 20.3 s per 2^20-client pass (profiles/r16/hh_ab.txt);
+//   0: re-read for every start node straight from the key batch's
+//     [key][level] rows (scattered 16-byte reads, ~60 TB of fetches per
+//     2^20 pass), 4 waves per SIMD.
+#ifndef DPF_HH_KEYS_MODE
+#define DPF_HH_KEYS_MODE 2
+#endif
+#define DPF_HH_KEYS_HOIST (DPF_HH_KEYS_MODE == 1)
+#ifndef DPF_HH_KEYS_WAVES
+#define DPF_HH_KEYS_WAVES (DPF_HH_KEYS_HOIST ? 3 : 4)
+#endif
+constexpr int kHHKeysBlock = 256 * DPF_HH_KEYS_WAVES;
+struct HHKeysLds {
+  uint32_t tab[kTabWords];
+#if DPF_HH_STASH
+  uint4 stash[2][kHHKeysBlock];  // [leaf 2 / 3][thread]: seed | control bit
+#endif
+};
+
+__device__ __forceinline__ uint4 cw_u4(const dpf_block& c) {
+  return make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
+                    (uint32_t)(c.high >> 32));
+}
+
+__global__ __launch_bounds__(kHHKeysBlock)
+__attribute__((amdgpu_waves_per_eu(DPF_HH_KEYS_WAVES, DPF_HH_KEYS_WAVES)))
+void hh_keys_kernel(HHKeysParams p) {
+  __shared__ HHKeysLds lds;
+  fill_tables(lds.tab);
+  __syncthreads();
+  const uint32_t lt = (threadIdx.x & 31) * 4u;
+  uint32_t m1;
+  asm volatile("v_mov_b32 %0, 0xff00" : "=v"(m1));
+  const LdsLookup lk{reinterpret_cast<const char*>(lds.tab),
+                     {lt, lt + 128u, lt + 65536u, lt + 65664u}, m1,
+                     KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), KeyRef{}}};
+  const int64_t K = p.num_keys, U = p.num_starts;
+  const int lane = (int)(threadIdx.x & 63);
+  const int64_t waves_per_block = kHHKeysBlock / 64;
+  const int64_t wave0 = (int64_t)blockIdx.x * waves_per_block +
+                        __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nl = p.nl;
+  const Div32 div0 = p.div[0], div1 = p.div[1];
+  for (int64_t w = wave0; w < p.num_waves; w += (int64_t)gridDim.x * waves_per_block) {
+    const int64_t grp = w / p.u_ranges;
+    const int64_t rng = w - grp * p.u_ranges;
+    const int64_t k_raw = grp * 64 + lane;
+    const bool valid = k_raw < K;
+    const int64_t k = valid ? k_raw : K - 1;
+    const int64_t cwi = k * p.cw_stride + p.cw_level;
+    const dpf_block* vc = p.vcw + k * p.vcw_stride;
+#if DPF_HH_KEYS_HOIST
+    // The key's two levels of correction words, value correction and party.
+    const uint4 key_cs0 = cw_u4(p.cw_seed[cwi]), key_cs1 = cw_u4(p.cw_seed[cwi + 1]);
+    const uint32_t key_cc = (uint32_t)(p.cw_left[cwi] & 1) | ((uint32_t)(p.cw_right[cwi] & 1) << 1) |
+                            ((uint32_t)(p.cw_left[cwi + 1] & 1) << 2) |
+                            ((uint32_t)(p.cw_right[cwi + 1] & 1) << 3) |
+                            ((uint32_t)(p.party[k] & 1) << 4);
+    const uint32_t key_corr0 = (uint32_t)vc[0].low, key_corr1 = nl > 1 ? (uint32_t)vc[1].low : 0u;
+#endif
+    const int64_t u_begin = rng * p.u_per_range;
+    const int64_t u_end = u_begin + p.u_per_range < U ? u_begin + p.u_per_range : U;
+    const int64_t len = u_end - u_begin;
+    const int64_t rot = len > 0 ? grp % len : 0;
+    for (int64_t i = 0; i < len; ++i) {
+      int64_t ui = i + rot;
+      if (ui >= len) ui -= len;
+      const int64_t u = u_begin + ui;   // wave-uniform
+      const int64_t par = p.parent[u];
+      Block4 s = load_block(p.seeds_in + par * K + k);
+      uint32_t t;
+      if (p.ctrl_in) {
+        t = p.ctrl_in[par * K + k] & 1u;
+      } else {
+        t = s.w0 & 1u;
+        s.w0 &= ~1u;
+      }
+      if (p.save_index) {
+        const int64_t save = p.save_index[u];
+        if (save >= 0 && valid) {
+          store_block(p.seeds_out + save * K + k, s);
+          p.ctrl_out[save * K + k] = (uint8_t)t;
+        }
+      }
+      // Two tree levels (cc:304-347): children (ILP2), grandchildren (ILP4);
+      // leaf order 0..3 = LL, LR, RL, RR.
+      Block4 c0, c1;
+      uint32_t t0, t1;
+      {
+#if DPF_HH_KEYS_HOIST
+        const uint4 cs0 = key_cs0;
+        const uint32_t cc0 = key_cc & 3u;
+#elif DPF_HH_KEYS_MODE == 2
+        const uint4 cs0 = p.key_tab[k];
+        const uint32_t cc0 = p.key_tab[2 * K + k].x & 3u;
+#else
+        const uint4 cs0 = cw_u4(p.cw_seed[cwi]);
+        const uint32_t cc0 = (uint32_t)(p.cw_left[cwi] & 1) | ((uint32_t)(p.cw_right[cwi] & 1) << 1);
+#endif
+        children_step(lk, lk.ks.l, lk.ks.r, s, t, cs0, cc0, c0, t0, c1, t1);
+      }
+      Block4 L[4];
+      uint32_t tl[4];
+      {
+#if DPF_HH_KEYS_HOIST
+        const uint4 cs1 = key_cs1;
+        const uint32_t cc1 = (key_cc >> 2) & 3u;
+#elif DPF_HH_KEYS_MODE == 2
+        const uint4 cs1 = p.key_tab[K + k];
+        const uint32_t cc1 = (p.key_tab[2 * K + k].x >> 2) & 3u;
+#else
+        const uint4 cs1 = cw_u4(p.cw_seed[cwi + 1]);
+        const uint32_t cc1 =
+            (uint32_t)(p.cw_left[cwi + 1] & 1) | ((uint32_t)(p.cw_right[cwi + 1] & 1) << 1);
+#endif
+        children_step_x2(lk, lk.ks.l, lk.ks.r, c0, t0, c1, t1, cs1, cc1, L, tl);
+      }
+      if (p.leaf_seeds && valid) {
+        int4 sl = make_int4((int)(u << 2), (int)(u << 2) + 1, (int)(u << 2) + 2, (int)(u << 2) + 3);
+        if (p.leaf_slot) sl = *reinterpret_cast<const int4*>(p.leaf_slot + (u << 2));
+        const int slot[4] = {sl.x, sl.y, sl.z, sl.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          Block4 c = L[j];
+          c.w0 |= tl[j];
+          store_block(p.leaf_seeds + slot[j] * K + k, c);
+        }
+      }
+#if DPF_HH_STASH
+      lds.stash[0][threadIdx.x] = make_uint4(L[2].w0 | tl[2], L[2].w1, L[2].w2, L[2].w3);
+      lds.stash[1][threadIdx.x] = make_uint4(L[3].w0 | tl[3], L[3].w1, L[3].w2, L[3].w3);
+#endif
+      // Value hashes (cc:500-524), sampling, correction, party negation.
+      uint32_t v[8];   // [leaf * 2 + element]
+      // Leaves 0 and 1 are sampled before leaves 2 and 3 are hashed; the
+      // correction and negation of all four wait until after (the value
+      // correction and party are read there): fewer live registers across
+      // the second pair's hashes.
+      uint32_t tb = tl[0] | (tl[1] << 1);
+      const UniformRK rk[4] = {UniformRK{lk.ks.v}, UniformRK{lk.ks.v}, UniformRK{lk.ks.v},
+                               UniformRK{lk.ks.v}};
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+#if DPF_HH_STASH
+        if (pr == 1) {
+          // Same thread wrote these: no barrier needed.
+          const uint4 a = lds.stash[0][threadIdx.x], c = lds.stash[1][threadIdx.x];
+          tb |= ((a.x & 1u) << 2) | ((c.x & 1u) << 3);
+          L[2] = Block4{a.x & ~1u, a.y, a.z, a.w};
+          L[3] = Block4{c.x & ~1u, c.y, c.z, c.w};
+        }
+#else
+        if (pr == 1) tb |= (tl[2] << 2) | (tl[3] << 3);
+#endif
+        Block4 h[4];
+        if (p.b == 2) {
+          hash_leaf_pair(lk, lk.ks.v, L[2 * pr], L[2 * pr + 1], h);
+        } else {
+          Block4 two[2] = {L[2 * pr], L[2 * pr + 1]};
+          dpf_aes::mmo_hashN<2>(two, lk, rk);
+          h[0] = two[0];
+          h[2] = two[1];
+          h[1] = h[3] = Block4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int leaf = 2 * pr + j;
+          sample2_nl(nl, div0, div1, h[2 * j], h[2 * j + 1].w0, &v[leaf * 2]);
+        }
+      }
+      {
+#if DPF_HH_KEYS_HOIST
+        const uint32_t corr[2] = {key_corr0, key_corr1};
+        const bool neg = (key_cc & 16u) != 0;
+#elif DPF_HH_KEYS_MODE == 2
+        const uint4 meta = p.key_tab[2 * K + k];
+        const uint32_t corr[2] = {meta.y, meta.z};
+        const bool neg = (meta.x & 16u) != 0;
+#else
+        const uint32_t corr[2] = {(uint32_t)vc[0].low, nl > 1 ? (uint32_t)vc[1].low : 0u};
+        const bool neg = (p.party[k] & 1u) != 0;
+#endif
+#pragma unroll
+        for (int leaf = 0; leaf < 4; ++leaf) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const uint32_t n = e ? div1.n : div0.n;
+            uint32_t r = v[leaf * 2 + e];
+            if ((tb >> leaf) & 1u) r = mod_add(r, corr[e], n);   // int_mod_n.h:116-120
+            if (neg) r = r == 0 ? 0u : n - r;                     // int_mod_n.h:208-218
+            v[leaf * 2 + e] = (e < nl && valid) ? r : 0u;
+          }
+        }
+      }
+      const uint32_t total = wave_sum8_mod(v, div0.n, nl > 1 ? div1.n : div0.n);
+      const int idx = lane >> 3, e = idx & 1;
+      if ((lane & 7) == 0 && e < nl && total)
+        atomicAdd(p.sums + ((u << 2) + (idx >> 1)) * nl + e, (unsigned long long)total);
+    }
+  }
+}
+
+// The per-call key table of hh_keys_kernel (DPF_HH_KEYS_MODE 2): key k's
+// correction words of levels cw_level, cw_level + 1 and its control-bit
+// corrections, value correction and party, index-major so that a wave of 64
+// keys reads each part as one 1 KiB access.
+__global__ void hh_key_table_kernel(int64_t K, int cw_level, int cw_stride,
+                                    const dpf_block* __restrict__ cw_seed,
+                                    const uint8_t* __restrict__ cw_left,
+                                    const uint8_t* __restrict__ cw_right,
+                                    const dpf_block* __restrict__ vcw, int vcw_stride, int nl,
+                                    const uint8_t* __restrict__ party, uint4* __restrict__ tab) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < K;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cwi = k * cw_stride + cw_level;
+    tab[k] = cw_u4(cw_seed[cwi]);
+    tab[K + k] = cw_u4(cw_seed[cwi + 1]);
+    const uint32_t cc = (uint32_t)(cw_left[cwi] & 1) | ((uint32_t)(cw_right[cwi] & 1) << 1) |
+                        ((uint32_t)(cw_left[cwi + 1] & 1) << 2) |
+                        ((uint32_t)(cw_right[cwi + 1] & 1) << 3) | ((uint32_t)(party[k] & 1) << 4);
+    const dpf_block* vc = vcw + k * vcw_stride;
+    tab[2 * K + k] = make_uint4(cc, (uint32_t)vc[0].low, nl > 1 ? (uint32_t)vc[1].low : 0u, 0u);
+  }
+}
+
 }  // namespace
 
 namespace dpf_rt {
 
+int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
+  HHKeysParams p;
+  memset(&p, 0, sizeof(p));
+  p.num_keys = a.num_keys;
+  p.num_starts = a.num_starts;
+  const int64_t groups = (a.num_keys + 63) / 64;
+  // At least ~4 waves per wave slot of the chip: split the start nodes when
+  // there are few 64-key groups.
+  const int64_t want_waves = (int64_t)num_cus() * (kHHKeysBlock / 64) * 4;
+  int64_t ranges = (want_waves + groups - 1) / groups;
+  if (ranges > a.num_starts) ranges = a.num_starts;
+  if (ranges < 1) ranges = 1;
+  p.u_per_range = (a.num_starts + ranges - 1) / ranges;
+  p.u_ranges = (a.num_starts + p.u_per_range - 1) / p.u_per_range;
+  p.num_waves = groups * p.u_ranges;
+  p.cw_level = a.cw_level;
+  p.cw_stride = a.cw_stride;
+  p.nl = a.nl;
+  p.b = a.b;
+  p.seeds_in = a.seeds_in;
+  p.ctrl_in = a.ctrl_in;
+  p.parent = a.parent;
+  p.save_index = a.save_index;
+  p.seeds_out = a.seeds_out;
+  p.ctrl_out = a.ctrl_out;
+  p.cw_seed = a.cw_seed;
+  p.cw_left = a.cw_left;
+  p.cw_right = a.cw_right;
+  p.vcw = a.vcw;
+  p.vcw_stride = a.vcw_stride;
+  p.party = a.party;
+  p.sums = a.wide;
+  p.leaf_seeds = a.leaf_seeds;
+  p.leaf_slot = a.leaf_slot;
+  for (int i = 0; i < 2; ++i) p.div[i] = make_div32(a.mod[i < a.nl ? i : 0]);
+  p.rkl = expand_key(a.key_left);
+  p.rkr = expand_key(a.key_right);
+  p.rkv = expand_key(a.key_value);
+  int64_t grid = (p.num_waves * 64 + kHHKeysBlock - 1) / kHHKeysBlock;
+  if (grid > num_cus()) grid = num_cus();   // one 128 KiB-table workgroup per CU
+  if (grid < 1) grid = 1;
+  void* tab = nullptr;
+  if (DPF_HH_KEYS_MODE == 2) {
+    // Stream-ordered scratch (48 B per key), freed behind the kernel; the
+    // device's default pool keeps it for the next level's call.
+    static const bool pool_kept = [] {
+      int dev = 0;
+      hipMemPool_t pool;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess)
+        return false;
+      uint64_t keep = UINT64_MAX;
+      return hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) == hipSuccess;
+    }();
+    (void)pool_kept;
+    HIP_TRY(hipMallocAsync(&tab, (size_t)a.num_keys * 3 * sizeof(uint4), s));
+    int64_t g = (a.num_keys + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(hh_key_table_kernel, dim3((unsigned)g), dim3(256), 0, s, a.num_keys,
+                       a.cw_level, a.cw_stride, a.cw_seed, a.cw_left, a.cw_right, a.vcw,
+                       a.vcw_stride, a.nl, a.party, static_cast<uint4*>(tab));
+    p.key_tab = static_cast<const uint4*>(tab);
+  }
+  hipLaunchKernelGGL(hh_keys_kernel, dim3((unsigned)grid), dim3(kHHKeysBlock), 0, s, p);
+  const hipError_t e = hipGetLastError();
+  if (tab) HIP_TRY(hipFreeAsync(tab, s));
+  HIP_TRY(e);
+  return kOk;
+}
+
 int launch_hh_level(const HHLevelArgs& a, hipStream_t s) {
   if (a.nl < 1 || a.nl > 2 || (a.b != 1 && a.b != 2) || (a.nl == 2 && a.b != 2))
     return fail(kUnimplemented, "hh_level_kernel: unsupported value type");
+  if (a.index_major) return launch_hh_keys(a, s);
   HHParams p;
   memset(&p, 0, sizeof(p));
   p.num_keys = a.num_keys;

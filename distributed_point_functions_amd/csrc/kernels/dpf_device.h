@@ -1213,9 +1213,11 @@ inline RoundKeys xor_keys(const RoundKeys& a, const RoundKeys& b) {
 // Turns the 192-bit exact per-leaf sums into group elements and packs them:
 // plain integers keep the low `bits`, XorWrapper is already reduced, IntModN
 // takes the sum mod N (int_mod_n.h:116-120).
+// `words` = 3: [point][leaf][3] 192-bit sums; 1: one uint64 per [point][leaf]
+// (hh_keys_kernel, whose sums of < 2^32 values over <= 2^31 keys fit).
 __global__ void finalize_sums_kernel(int64_t num_points, dpf_value_desc d,
                                      const unsigned long long* __restrict__ wide,
-                                     char* __restrict__ out) {
+                                     char* __restrict__ out, int words) {
   const int nl = d.num_leaves;
   int esz = 0;
   for (int k = 0; k < nl; ++k) esz += d.bits[k] >> 3;
@@ -1223,14 +1225,15 @@ __global__ void finalize_sums_kernel(int64_t num_points, dpf_value_desc d,
        i += (int64_t)gridDim.x * blockDim.x) {
     char* o = out + i * esz;
     for (int k = 0; k < nl; ++k) {
-      const unsigned long long* w = wide + (i * nl + k) * 3;
-      u128 v = ((u128)w[1] << 64) | w[0];
+      const unsigned long long* w = wide + (i * nl + k) * words;
+      const unsigned long long w2 = words == 3 ? w[2] : 0ull;
+      u128 v = words == 3 ? (((u128)w[1] << 64) | w[0]) : (u128)w[0];
       if (d.kind[k] == DPF_LEAF_INTMODN) {
         const u128 n = ((u128)d.mod_high[k] << 64) | d.mod_low[k];
         // r = (w2 * 2^128 + v) mod n, one bit at a time (r < n throughout).
         u128 r = 0;
         for (int b = 191; b >= 0; --b) {
-          const unsigned bit = b >= 128 ? (unsigned)((w[2] >> (b - 128)) & 1)
+          const unsigned bit = b >= 128 ? (unsigned)((w2 >> (b - 128)) & 1)
                                         : (unsigned)((v >> b) & 1);
           r = (r >= n - r) ? r - (n - r) : r + r;  // 2r mod n
           if (bit) r = (r >= n - 1) ? 0 : r + 1;   // +1 mod n

@@ -1734,6 +1734,16 @@ int dpf_hip_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
   HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
   return kOk;
 }
+int dpf_hip_memcpy_d2h_strided(void* dst, const void* src, size_t elem_bytes,
+                               size_t src_stride_bytes, int64_t count, void* stream) {
+  if (count < 0 || src_stride_bytes < elem_bytes) return fail(kInvalidArgument, "bad sizes");
+  if (count == 0 || elem_bytes == 0) return kOk;
+  if (!dst || !src) return fail(kInvalidArgument, "NULL pointer");
+  HIP_TRY(hipMemcpy2DAsync(dst, elem_bytes, src, src_stride_bytes, elem_bytes, (size_t)count,
+                           hipMemcpyDeviceToHost, (hipStream_t)stream));
+  HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+  return kOk;
+}
 int dpf_hip_memcpy_d2h_staged(void* dst, const void* src, size_t bytes,
                               void (*before_chunk)(void* ctx, size_t bytes_ready), void* ctx,
                               void* stream) {
@@ -2172,7 +2182,7 @@ int dpf_hip_eval_points_sum(int64_t num_keys, int64_t num_points, int num_levels
   int64_t g = (num_points + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(finalize_sums_kernel, dim3((unsigned)g), dim3(256), 0, s, num_points, *desc,
-                     reinterpret_cast<const unsigned long long*>(workspace), (char*)out);
+                     reinterpret_cast<const unsigned long long*>(workspace), (char*)out, 3);
   HIP_TRY(hipGetLastError());
   return kOk;
 }

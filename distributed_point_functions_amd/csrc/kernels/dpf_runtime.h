@@ -50,6 +50,12 @@ struct HHLevelArgs {
   dpf_block* leaf_seeds;
   int64_t leaf_stride;
   const int32_t* leaf_slot;  // NULL: leaf i of start node u at slot (u << 2) + i
+  // 0: per-key tables key-major, element (k, j) at k*stride + j; sums into
+  //    the 192-bit [slot][leaf][3] workspace (hh_level_kernel).
+  // 1: index-major, element (k, j) at j*num_keys + k (the device batch
+  //    context's layout); lanes are keys (hh_keys_kernel) and the sums go to
+  //    one uint64 per [slot][leaf] (finalize with words == 1).
+  int index_major;
   int nl, b;
   uint32_t mod[2];
   const dpf_aes_key* key_left;
@@ -57,6 +63,7 @@ struct HHLevelArgs {
   const dpf_aes_key* key_value;
 };
 int launch_hh_level(const HHLevelArgs& a, hipStream_t s);
+int launch_hh_keys(const HHLevelArgs& a, hipStream_t s);   // index_major == 1
 
 }  // namespace dpf_rt
 

@@ -85,8 +85,10 @@ class DeviceKeyBatch {
 // (the heavy-hitters pattern of config 5b), so the context holds one shared
 // list of partial-evaluation prefixes (tree indices at depth
 // hierarchy_to_tree[partial_evaluations_level]) and, per key, the seed and
-// control bit at each of them -- key-major, [key][prefix] -- instead of a
-// protobuf repeated field per key.  Created by
+// control bit at each of them -- index-major, [prefix][key], so 64
+// consecutive keys at one prefix are one 1 KiB access (DPF_BATCH_KEY_MAJOR=1
+// at creation: key-major [key][prefix]) -- instead of a protobuf repeated
+// field per key.  Created by
 // DistributedPointFunction::CreateBatchEvaluationContext; serialized lazily to
 // a per-key EvaluationContext proto by ExportEvaluationContext.
 class DeviceBatchContext {
@@ -100,9 +102,12 @@ class DeviceBatchContext {
   int partial_evaluations_level() const { return partial_evaluations_level_; }
   // Shared partial-evaluation prefixes (tree indices), in evaluation order.
   const std::vector<uint128>& partial_prefixes() const { return partial_prefixes_; }
-  // Device arrays [num_keys][partial_prefixes().size()].
+  // Device arrays [partial_prefixes().size()][num_keys] (index_major()), else
+  // [num_keys][partial_prefixes().size()].
   const dpf_block* partial_seeds() const { return static_cast<const dpf_block*>(seeds_); }
   const uint8_t* partial_control() const { return static_cast<const uint8_t*>(ctrl_); }
+  // Layout of the partial evaluations and the expansion cache.
+  bool index_major() const { return index_major_; }
   // Back to the state CreateBatchEvaluationContext returns, keeping the
   // device allocations for the next pass over the hierarchy; with
   // `release_expansion_cache` the expansion cache (up to K x 4096 x 16 B per
@@ -158,7 +163,9 @@ class DeviceBatchContext {
   void* next_seeds_ = nullptr;  // written by the next evaluation, then swapped in
   void* next_ctrl_ = nullptr;
   size_t next_seeds_cap_ = 0, next_ctrl_cap_ = 0;
-  // Expansion cache: the tree leaves of the last call ([key][leaf_stride_]),
+  bool index_major_ = true;
+  // Expansion cache: the tree leaves of the last call ([leaf_stride_][key]
+  // index-major, else [key][leaf_stride_]),
   // i.e. the next call's tree nodes (DistributedPointFunction's batched
   // EvaluateUntil reads its start seeds from it instead of walking down
   // from the partial evaluations two calls back).  leaf_de_: levels from a

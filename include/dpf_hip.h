@@ -383,12 +383,45 @@ int dpf_hip_eval_prefix_batch_cached_slots(
     const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
     dpf_block* leaf_cache, int64_t leaf_stride, const int32_t* leaf_slot, void* stream);
 
+/* dpf_hip_eval_prefix_batch_cached_slots with the layout of its per-key
+ * tables chosen.  index_major == 0 is exactly that function: element (key k,
+ * slot j) of seeds_in / control_in, seeds_out / control_out and leaf_cache at
+ * k*stride + j.  index_major == 1 puts it at j*num_keys + k for all three
+ * (in_stride, out_stride and leaf_stride then only give the slots per key):
+ * the layout of the device batch context (DeviceBatchContext), in which 64
+ * consecutive keys at one slot are one 1 KiB access.  With index_major == 1
+ * the heavy-hitters steady state (no walk, two expanded levels, sum mode,
+ * IntModN<uint32_t> tuples) runs with lanes = keys ("hh_keys" in
+ * dpf_hip_last_batch_kernel); outputs are identical in both layouts. */
+int dpf_hip_eval_prefix_batch_layout(
+    int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
+    int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
+    const dpf_block* seeds_in, const uint8_t* control_in, int64_t in_stride,
+    const int32_t* parent, const dpf_block* path, const int32_t* save_index, dpf_block* seeds_out,
+    uint8_t* control_out, int64_t out_stride, const dpf_block* cw_seed, const uint8_t* cw_left,
+    const uint8_t* cw_right, const dpf_aes_key* key_left, const dpf_aes_key* key_right,
+    const dpf_aes_key* key_value, const dpf_value_desc* desc, int elements_per_leaf,
+    const dpf_block* value_correction, int sum, uint64_t* workspace, void* out,
+    dpf_block* leaf_cache, int64_t leaf_stride, const int32_t* leaf_slot, int index_major,
+    void* stream);
+
 /* seeds_out[k*num_rows + i] / control_out[k*num_rows + i] = the seed (bit 0
  * cleared) and control bit (bit 0) of cache[k*cache_stride + slot[i]]: a
  * call's start seeds from the previous call's expansion cache. */
 int dpf_hip_gather_seeds(int64_t num_keys, int64_t num_rows, const int64_t* slot,
                          const dpf_block* cache, int64_t cache_stride, dpf_block* seeds_out,
                          uint8_t* control_out, void* stream);
+/* dpf_hip_gather_seeds with index_major == 1: seeds_out / control_out[i*num_keys
+ * + k] from cache[slot[i]*num_keys + k] (cache_stride unused). */
+int dpf_hip_gather_seeds_layout(int64_t num_keys, int64_t num_rows, const int64_t* slot,
+                                const dpf_block* cache, int64_t cache_stride, dpf_block* seeds_out,
+                                uint8_t* control_out, int index_major, void* stream);
+
+/* Device-to-host copy of `count` elements of `elem_bytes` each, element i
+ * read at src + i*src_stride_bytes and written packed to dst (a column of an
+ * index-major table: one key's partial evaluations, ExportEvaluationContext). */
+int dpf_hip_memcpy_d2h_strided(void* dst, const void* src, size_t elem_bytes,
+                               size_t src_stride_bytes, int64_t count, void* stream);
 
 /* Largest expand_levels dpf_hip_eval_prefix_batch accepts for this value type
  * (register-resident subtree), or -1 if `sum` mode is not available. */

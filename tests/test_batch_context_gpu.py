@@ -410,9 +410,11 @@ def test_reset_releases_expansion_cache():
 
 def test_heavy_hitters_levels_run_the_lean_kernel(monkeypatch):
     """Cached heavy-hitters levels (start seeds from the expansion cache, two
-    expanded levels, Tuple<IntModN32 x2> sums) run hh_level_kernel
-    (dpf_batch_hh.hip); DPF_BATCH_NO_LEAN=1 runs the general kernel.  Both
-    equal the oracle (checked by _run), and each other."""
+    expanded levels, Tuple<IntModN32 x2> sums) run hh_keys_kernel (lanes =
+    keys, index-major tables; dpf_batch_hh.hip); DPF_BATCH_KEY_MAJOR=1 runs
+    r15's hh_level_kernel (lanes = start nodes, key-major tables) and
+    DPF_BATCH_NO_LEAN=1 the general kernel.  All equal the oracle (checked by
+    _pressure_run), and each other."""
     from distributed_point_functions_amd import hip_abi as H
     levels, plan = HH5
     seen = []
@@ -422,7 +424,35 @@ def test_heavy_hitters_levels_run_the_lean_kernel(monkeypatch):
             seen.append(H.last_batch_kernel())
     _pressure_run(levels, plan, 45, True, seed=97, arm=arm)
     seen.append(H.last_batch_kernel())
-    assert seen[-1] == "hh_level", seen   # the last (cached) level
+    assert seen[-1] == "hh_keys", seen   # the last (cached) level
+    monkeypatch.setenv("DPF_BATCH_KEY_MAJOR", "1")
+    _pressure_run(levels, plan, 45, True, seed=97)
+    assert H.last_batch_kernel() == "hh_level"
+    monkeypatch.delenv("DPF_BATCH_KEY_MAJOR")
     monkeypatch.setenv("DPF_BATCH_NO_LEAN", "1")
     _pressure_run(levels, plan, 45, True, seed=97)
     assert H.last_batch_kernel() == "batch_level/mod32"
+
+
+@pytest.mark.parametrize("levels,plan", CASES[:4] + CASES[-3:], ids=lambda x: str(x)[:60])
+@pytest.mark.parametrize("mode", ["default", "permute", "gather"])
+def test_batch_key_major_layout(levels, plan, mode, monkeypatch):
+    """DPF_BATCH_KEY_MAJOR=1: the r15 key-major context tables ([key][slot])
+    with every cache mode -- same outputs and exported contexts as the
+    index-major default."""
+    monkeypatch.setenv("DPF_BATCH_KEY_MAJOR", "1")
+    if mode != "default":
+        monkeypatch.setenv("DPF_BATCH_CACHE_MODE", mode)
+    _run(levels, plan, 37, True, seed=len(levels) + 19)
+
+
+@pytest.mark.parametrize("n_keys", [63, 64, 65, 1000])
+@pytest.mark.parametrize("mode", ["default", "permute", "gather"])
+def test_hh_keys_kernel_key_groups(n_keys, mode, monkeypatch):
+    """Lanes = keys: ragged last 64-key group, one group, and enough groups
+    that each wave takes a range of start nodes -- sums and exported contexts
+    equal the oracle in every cache mode."""
+    if mode != "default":
+        monkeypatch.setenv("DPF_BATCH_CACHE_MODE", mode)
+    levels, plan = HH5
+    _pressure_run(levels, plan, n_keys, True, seed=n_keys + 3)
