@@ -218,9 +218,37 @@ void DeviceBatchContext::Reset(bool release_expansion_cache) {
 }
 
 DeviceBatchContext::~DeviceBatchContext() {
+  if (tables_pending_) (void)dpf_hip_event_sync(tables_event_);
+  if (tables_event_) dpf_hip_event_destroy(tables_event_);
+  if (pinned_tables_) dpf_hip_host_free(pinned_tables_);
   for (void* p : {seeds_, ctrl_, next_seeds_, next_ctrl_, parent_, path_, save_, offsets_,
                   workspace_, stage_, stage2_, leaf_seeds_, leaf_spare_, slots_, leaf_slot_})
     if (p) dpf_hip_free(p);
+}
+
+Status DeviceBatchContext::StageTables(size_t bytes) {
+  if (tables_pending_) {
+    HIP_RETURN_IF_ERROR(dpf_hip_event_sync(tables_event_));
+    tables_pending_ = false;
+  }
+  if (pinned_tables_cap_ >= bytes && pinned_tables_) return OkStatus();
+  if (pinned_tables_) dpf_hip_host_free(pinned_tables_);
+  pinned_tables_ = nullptr;
+  pinned_tables_cap_ = 0;
+  const size_t want = std::max<size_t>(bytes + bytes / 2, size_t{1} << 16);
+  if (dpf_hip_host_alloc(&pinned_tables_, want) != 0) {
+    pinned_tables_ = nullptr;
+    return ResourceExhaustedError("Memory allocation error");
+  }
+  pinned_tables_cap_ = want;
+  return OkStatus();
+}
+
+Status DeviceBatchContext::TablesSent(void* stream) {
+  if (!tables_event_) HIP_RETURN_IF_ERROR(dpf_hip_event_create(&tables_event_));
+  HIP_RETURN_IF_ERROR(dpf_hip_event_record(tables_event_, stream));
+  tables_pending_ = true;
+  return OkStatus();
 }
 
 StatusOr<std::unique_ptr<DeviceBatchContext>> DistributedPointFunction::CreateBatchEvaluationContext(
@@ -508,20 +536,25 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   };
 
   clk.mark(1);
-  // Start-node tables: u = tree index i * 2^s + sub.  Host staging buffers
-  // are reused across calls (no page faults on 1 M-entry levels).
-  static thread_local std::vector<int32_t> tl_parent, tl_save;
-  static thread_local std::vector<dpf_block> tl_path;
-  // Plain references: the worker threads below must write the CALLING
-  // thread's buffers, not their own thread_local instances.
-  std::vector<int32_t>& parent = tl_parent;
-  std::vector<int32_t>& save = tl_save;
-  std::vector<dpf_block>& path = tl_path;
-  if (static_cast<int64_t>(parent.size()) < U) {
-    parent.resize(U);
-    save.resize(U);
-    path.resize(U);
-  }
+  // Start-node tables (u = tree index i * 2^s + sub) and the output gather's
+  // offsets, built in ONE page-locked image on host threads and sent with one
+  // asynchronous H2D into one device buffer: parent[U] int32 | save[U] int32
+  // (only with s > 0: with s == 0 start node u IS tree index u, save_index
+  // NULL) | path[U] (only when the kernel walks, Wk + s > 0) | offsets[P]
+  // int64 (non-identity gathers).  Three synchronous pageable copies of
+  // 24 MiB had cost a 1 M-prefix level (config 5a) milliseconds.
+  const bool need_path = Wk + s > 0;
+  const bool need_save = s > 0;
+  auto align = [](size_t b) { return (b + 255) & ~size_t{255}; };
+  const size_t off_save = align(static_cast<size_t>(U) * sizeof(int32_t));
+  const size_t off_path = off_save + (need_save ? align(static_cast<size_t>(U) * sizeof(int32_t)) : 0);
+  const size_t off_offsets = off_path + (need_path ? align(static_cast<size_t>(U) * sizeof(dpf_block)) : 0);
+  const size_t tables_bytes = off_offsets + (identity ? 0 : static_cast<size_t>(P) * sizeof(int64_t));
+  DPF_RETURN_IF_ERROR(ctx.StageTables(tables_bytes));
+  char* img = static_cast<char*>(ctx.pinned_tables_);
+  int32_t* parent = reinterpret_cast<int32_t*>(img);
+  int32_t* save = need_save ? reinterpret_cast<int32_t*>(img + off_save) : nullptr;
+  dpf_block* path = need_path ? reinterpret_cast<dpf_block*>(img + off_path) : nullptr;
   const uint128 w1_mask = Wk >= 128 ? ~uint128{0} : ((uint128{1} << Wk) - 1);
   dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
     for (int64_t i = lo; i < hi; ++i) {
@@ -534,18 +567,27 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
       for (int64_t sub = 0; sub < (int64_t{1} << s); ++sub) {
         const int64_t u = (i << s) + sub;
         parent[u] = start;
-        path[u] = ToBlock(s ? ((low << s) | static_cast<uint128>(sub)) : low);
-        save[u] = sub == 0 ? static_cast<int32_t>(i) : -1;
+        if (path) path[u] = ToBlock(s ? ((low << s) | static_cast<uint128>(sub)) : low);
+        if (save) save[u] = sub == 0 ? static_cast<int32_t>(i) : -1;
       }
     }
   });
+  if (!identity) {
+    int64_t* offsets = reinterpret_cast<int64_t*>(img + off_offsets);
+    dpf_internal::ParallelFor(P, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i)
+        offsets[i] = prefix_map[i].first * block + prefix_map[i].second * cnt;
+    });
+  }
   clk.mark(2);
-  DPF_RETURN_IF_ERROR(ensure(&ctx.parent_, &ctx.parent_cap_, U * sizeof(int32_t)));
-  DPF_RETURN_IF_ERROR(ensure(&ctx.path_, &ctx.path_cap_, U * sizeof(dpf_block)));
-  DPF_RETURN_IF_ERROR(ensure(&ctx.save_, &ctx.save_cap_, U * sizeof(int32_t)));
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.parent_, parent.data(), U * sizeof(int32_t), stream));
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.path_, path.data(), U * sizeof(dpf_block), stream));
-  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.save_, save.data(), U * sizeof(int32_t), stream));
+  DPF_RETURN_IF_ERROR(ensure(&ctx.parent_, &ctx.parent_cap_, tables_bytes));
+  HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d_async(ctx.parent_, img, tables_bytes, stream));
+  DPF_RETURN_IF_ERROR(ctx.TablesSent(stream));
+  char* dtab = static_cast<char*>(ctx.parent_);
+  const int32_t* d_parent = reinterpret_cast<const int32_t*>(dtab);
+  const int32_t* d_save = need_save ? reinterpret_cast<const int32_t*>(dtab + off_save) : nullptr;
+  const dpf_block* d_path = need_path ? reinterpret_cast<const dpf_block*>(dtab + off_path) : nullptr;
+  const int64_t* d_offsets = identity ? nullptr : reinterpret_cast<const int64_t*>(dtab + off_offsets);
   if (update_ctx || gather) {
     DPF_RETURN_IF_ERROR(ensure(&ctx.next_seeds_, &ctx.next_seeds_cap_,
                                                    K * T * sizeof(dpf_block)));
@@ -579,15 +621,6 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.leaf_slot_, leaf_slot.data(), bytes, stream));
     ctx.leaf_level_ = -1;  // rewritten in place by this call's kernel
   }
-  std::vector<int64_t> offsets;
-  if (!identity) {
-    offsets.resize(P);
-    for (int64_t i = 0; i < P; ++i)
-      offsets[i] = prefix_map[i].first * block + prefix_map[i].second * cnt;
-    DPF_RETURN_IF_ERROR(
-        ensure(&ctx.offsets_, &ctx.offsets_cap_, P * sizeof(int64_t)));
-    HIP_RETURN_IF_ERROR(dpf_hip_memcpy_h2d(ctx.offsets_, offsets.data(), P * sizeof(int64_t), stream));
-  }
 
   clk.mark(3);
   const dpf_aes_key kl = AesKey(kPrgKeyLeft), kr = AesKey(kPrgKeyRight), kv = AesKey(kPrgKeyValue);
@@ -606,8 +639,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     return FromHip(dpf_hip_eval_prefix_batch_layout(
         K, U, Wk + s, update_ctx && !gather ? Wk : -1, E, cached ? Dprev : start_level,
         keys.num_levels(), keys.seed(), keys.party(), start_seeds, start_ctrl, start_stride,
-        static_cast<const int32_t*>(ctx.parent_), static_cast<const dpf_block*>(ctx.path_),
-        static_cast<const int32_t*>(ctx.save_), static_cast<dpf_block*>(ctx.next_seeds_),
+        d_parent, d_path, d_save, static_cast<dpf_block*>(ctx.next_seeds_),
         static_cast<uint8_t*>(ctx.next_ctrl_), T, keys.cw_seed(), keys.cw_left(), keys.cw_right(),
         &kl, &kr, &kv, &desc, cepb, keys.value_correction(hierarchy_level), sum_mode, workspace,
         out, static_cast<dpf_block*>(leaf_seeds), cache_stride,
@@ -624,7 +656,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
         &ctx.workspace_, &ctx.workspace_cap_, n_blk * f.leaves.size() * 3 * sizeof(uint64_t)));
     DPF_RETURN_IF_ERROR(launch(1, target, static_cast<uint64_t*>(ctx.workspace_)));
     if (!identity)
-      HIP_RETURN_IF_ERROR(dpf_hip_gather(P, cnt, esz, static_cast<const int64_t*>(ctx.offsets_),
+      HIP_RETURN_IF_ERROR(dpf_hip_gather(P, cnt, esz, d_offsets,
                                          ctx.stage_, device_out, stream));
   } else if (sum) {
     // Value types without an on-device key sum in the kernel: per-key rows,
@@ -638,7 +670,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     }
     HIP_RETURN_IF_ERROR(dpf_hip_sum_rows(K, n_blk, &desc, ctx.stage_, target, stream));
     if (!identity)
-      HIP_RETURN_IF_ERROR(dpf_hip_gather(P, cnt, esz, static_cast<const int64_t*>(ctx.offsets_),
+      HIP_RETURN_IF_ERROR(dpf_hip_gather(P, cnt, esz, d_offsets,
                                          ctx.stage2_, device_out, stream));
   } else {
     void* target = device_out;
@@ -649,7 +681,7 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
     DPF_RETURN_IF_ERROR(launch(0, target, nullptr));
     if (!identity)
       HIP_RETURN_IF_ERROR(dpf_hip_gather_batched(K, n_blk, P, cnt, esz,
-                                                 static_cast<const int64_t*>(ctx.offsets_),
+                                                 d_offsets,
                                                  ctx.stage_, device_out, stream));
   }
 

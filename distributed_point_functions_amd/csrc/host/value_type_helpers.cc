@@ -426,10 +426,17 @@ class WorkerPool {
     for (int i = 0; i < workers; ++i) threads_.emplace_back([this] { Loop(); });
   }
   int workers() const { return static_cast<int>(threads_.size()); }
-  // False if another thread's job is running.
+  // False if another thread's job is running.  The submitting thread is
+  // marked (in_job) while it runs chunks, so a nested parallel loop inside a
+  // chunk runs inline instead of try_lock-ing submit_, which it already owns
+  // (undefined behaviour for a std::mutex).
   bool TryRun(int chunks, const std::function<void(int)>& fn) {
     std::unique_lock<std::mutex> submit(submit_, std::try_to_lock);
     if (!submit.owns_lock()) return false;
+    struct JobMark {
+      JobMark() { in_job = true; }
+      ~JobMark() { in_job = false; }
+    } mark;
     {
       std::lock_guard<std::mutex> lock(mu_);
       fn_ = &fn;
@@ -452,6 +459,7 @@ class WorkerPool {
     return true;
   }
   static thread_local bool in_worker;
+  static thread_local bool in_job;   // this thread submitted the running job
 
  private:
   // Polls `done` for up to ~50 us (yielding the CPU between polls: a pause
@@ -508,30 +516,35 @@ class WorkerPool {
   std::vector<std::thread> threads_;
 };
 thread_local bool WorkerPool::in_worker = false;
+thread_local bool WorkerPool::in_job = false;
 
 // Never destroyed (its threads wait for work until the process exits); a
 // forked child starts a pool of its own (the parent's threads do not exist
-// there).
+// there).  fork() takes g_pool_mu first (prepare handler), so the child never
+// inherits it held by a thread that does not exist there; the child releases
+// it and forgets the parent's pool, whose mutexes may be held by such threads.
 std::atomic<WorkerPool*> g_pool{nullptr};
 std::mutex g_pool_mu;
 WorkerPool* Pool() {
   WorkerPool* p = g_pool.load();
   if (p) return p;
+  static bool atfork = [] {
+    pthread_atfork([] { g_pool_mu.lock(); }, [] { g_pool_mu.unlock(); },
+                   [] {
+                     g_pool_mu.unlock();
+                     g_pool.store(nullptr);
+                   });
+    return true;
+  }();
+  (void)atfork;
   std::lock_guard<std::mutex> lock(g_pool_mu);
-  if (!g_pool.load()) {
-    static bool atfork = [] {
-      pthread_atfork(nullptr, nullptr, [] { g_pool.store(nullptr); });
-      return true;
-    }();
-    (void)atfork;
-    g_pool.store(new WorkerPool(std::max(HostThreads() - 1, 1)));
-  }
+  if (!g_pool.load()) g_pool.store(new WorkerPool(std::max(HostThreads() - 1, 1)));
   return g_pool.load();
 }
 }  // namespace
 
 void RunOnPool(int chunks, const std::function<void(int)>& fn) {
-  if (chunks <= 1 || WorkerPool::in_worker) {
+  if (chunks <= 1 || WorkerPool::in_worker || WorkerPool::in_job) {
     for (int c = 0; c < chunks; ++c) fn(c);
     return;
   }

@@ -470,7 +470,8 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
     const int64_t k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
     const Block4 path = W > 0 ? load_block(p.path + u) : Block4{0, 0, 0, 0};
     const int32_t par = p.seeds_in ? p.parent[u] : 0;
-    const int32_t save = (p.save_after >= 0 && p.seeds_out) ? p.save_index[u] : -1;
+    const int32_t save = (p.save_after >= 0 && p.seeds_out)
+                             ? (p.save_index ? p.save_index[u] : (int32_t)u) : -1;
     typename V::Val acc[1 << MAXE];
 #pragma unroll
     for (int i = 0; i < (1 << MAXE); ++i) V::zero(acc[i]);
@@ -831,7 +832,7 @@ int dpf_hip_eval_prefix_batch_layout(
   if (num_keys > 0 && num_starts > 0) {
     if (!party || !value_correction || !key_left || !key_right || !key_value ||
         (!sum && !out) || (!seeds_in && !key_seed) || (seeds_in && !parent) ||
-        (walk_levels > 0 && !path) || (save_after >= 0 && (!seeds_out || !control_out || !save_index)) ||
+        (walk_levels > 0 && !path) || (save_after >= 0 && (!seeds_out || !control_out)) ||
         (walk_levels + expand_levels > 0 && (!cw_seed || !cw_left || !cw_right)))
       return fail(kInvalidArgument, "NULL pointer");
     BatchLevelParams p;
@@ -913,7 +914,8 @@ int dpf_hip_eval_prefix_batch_layout(
       a.ctrl_in = control_in;
       a.in_stride = in_stride;
       a.parent = parent;
-      a.save_index = (save_after == 0 && seeds_out) ? save_index : nullptr;
+      a.save = save_after == 0 && seeds_out;
+      a.save_index = save_index;
       a.seeds_out = seeds_out;
       a.ctrl_out = control_out;
       a.out_stride = out_stride;

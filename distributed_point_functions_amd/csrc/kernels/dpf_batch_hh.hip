@@ -216,7 +216,7 @@ void hh_level_kernel(HHParams p) {
     const int64_t k_begin = chunk * p.chunk_keys;
     const int64_t k_end = k_begin + p.chunk_keys < p.num_keys ? k_begin + p.chunk_keys : p.num_keys;
     const int32_t par = p.parent[u];
-    const int32_t save = p.save && valid ? p.save_index[u] : -1;
+    const int32_t save = p.save && valid ? (p.save_index ? p.save_index[u] : (int32_t)u) : -1;
     uint32_t acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = 0;
@@ -387,7 +387,8 @@ struct HHKeysParams {
   const dpf_block* seeds_in;   // [j][K]
   const uint8_t* ctrl_in;      // [j][K]; NULL: control bit in bit 0 of the seed
   const int32_t* parent;
-  const int32_t* save_index;   // NULL: no partial evaluations stored
+  int save;                    // 1: store each start node as the key's partial evaluation
+  const int32_t* save_index;   // NULL (with save): start node u at index u
   dpf_block* seeds_out;        // [save][K]
   uint8_t* ctrl_out;
   const dpf_block* cw_seed;    // [k][cw_stride] (the key batch's own layout)
@@ -460,6 +461,31 @@ struct HHKeysLds {
 #endif
 };
 
+// DPF_HH_NT=1: the streamed start seeds, cache leaves and partial
+// evaluations bypass L2 allocation (non-temporal), leaving L2 to the waves'
+// key tables (A/B variant).
+#ifndef DPF_HH_NT
+#define DPF_HH_NT 0
+#endif
+__device__ __forceinline__ Block4 stream_load(const dpf_block* p) {
+#if DPF_HH_NT
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return Block4{v.x, v.y, v.z, v.w};
+#else
+  return load_block(p);
+#endif
+}
+__device__ __forceinline__ void stream_store(dpf_block* p, Block4 b) {
+#if DPF_HH_NT
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = {b.w0, b.w1, b.w2, b.w3};
+  __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+#else
+  store_block(p, b);
+#endif
+}
+
 __device__ __forceinline__ uint4 cw_u4(const dpf_block& c) {
   return make_uint4((uint32_t)c.low, (uint32_t)(c.low >> 32), (uint32_t)c.high,
                     (uint32_t)(c.high >> 32));
@@ -510,7 +536,7 @@ void hh_keys_kernel(HHKeysParams p) {
       if (ui >= len) ui -= len;
       const int64_t u = u_begin + ui;   // wave-uniform
       const int64_t par = p.parent[u];
-      Block4 s = load_block(p.seeds_in + par * K + k);
+      Block4 s = stream_load(p.seeds_in + par * K + k);
       uint32_t t;
       if (p.ctrl_in) {
         t = p.ctrl_in[par * K + k] & 1u;
@@ -518,10 +544,10 @@ void hh_keys_kernel(HHKeysParams p) {
         t = s.w0 & 1u;
         s.w0 &= ~1u;
       }
-      if (p.save_index) {
-        const int64_t save = p.save_index[u];
+      if (p.save) {
+        const int64_t save = p.save_index ? p.save_index[u] : u;
         if (save >= 0 && valid) {
-          store_block(p.seeds_out + save * K + k, s);
+          stream_store(p.seeds_out + save * K + k, s);
           p.ctrl_out[save * K + k] = (uint8_t)t;
         }
       }
@@ -566,7 +592,7 @@ void hh_keys_kernel(HHKeysParams p) {
         for (int j = 0; j < 4; ++j) {
           Block4 c = L[j];
           c.w0 |= tl[j];
-          store_block(p.leaf_seeds + slot[j] * K + k, c);
+          stream_store(p.leaf_seeds + slot[j] * K + k, c);
         }
       }
 #if DPF_HH_STASH
@@ -692,6 +718,7 @@ int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
   p.seeds_in = a.seeds_in;
   p.ctrl_in = a.ctrl_in;
   p.parent = a.parent;
+  p.save = a.save;
   p.save_index = a.save_index;
   p.seeds_out = a.seeds_out;
   p.ctrl_out = a.ctrl_out;
@@ -757,7 +784,7 @@ int launch_hh_level(const HHLevelArgs& a, hipStream_t s) {
   p.num_threads = chunks * p.waves_per_chunk * 64;
   p.cw_level = a.cw_level;
   p.cw_stride = a.cw_stride;
-  p.save = a.save_index != nullptr;
+  p.save = a.save;
   p.nl = a.nl;
   p.b = a.b;
   p.seeds_in = a.seeds_in;

@@ -531,6 +531,22 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_small_kernel(Exp
   }
 }
 
+// Leaf policy of the tree-top pass (expand_top, below): expand_small_kernel's
+// last breadth-first level is not hashed; its nodes are stored as the start
+// seeds (seed, control bit) of the octet kernel's items.
+struct SeedLeaf {
+  dpf_block* seeds;
+  uint8_t* ctrl;
+  __device__ __forceinline__ void init() const {}
+  __device__ __forceinline__ void emit2(const LdsLookup&, KeyRef, Block4 s0, uint32_t t0, Block4 s1,
+                                        uint32_t t1, int64_t first, char*) const {
+    store_block(seeds + first, s0);
+    store_block(seeds + first + 1, s1);
+    ctrl[first] = (uint8_t)t0;
+    ctrl[first + 1] = (uint8_t)t1;
+  }
+};
+
 // PAIRED = false (launches below one wave per CU, never in sum mode): one
 // chain per lane, half = P, so a small call spreads over twice the CUs and each
 // wave's dependent AES chain issues half the LDS reads per round.
@@ -835,14 +851,89 @@ int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
   return kOk;
 }
 
+// Tree-top pass of an octet launch (r16).  Every octet-kernel item walks k0
+// levels from its start seed to its subtree root, one dependent AES per level
+// per lane: at config 2's 2^30 outputs 18 of each lane's ~6160 AES, but at
+// the 2^27-output shard a rank evaluates in an 8-GPU run (784 AES per lane)
+// the walk is ~4.5% of the kernel.  Instead, expand_small_kernel<SeedLeaf>
+// expands the top of the tree breadth-first -- each workgroup's wave 0 walks
+// to its subtree root in lane quads, then up to 11 levels through LDS, every
+// node hashed once -- and writes the 2^k0-per-start item roots (17 B each,
+// stream-ordered scratch); the octet kernel then starts at them (k0 = 0).
+// DPF_EXPAND_TOP=0 (read per launch) keeps the per-lane walk.
+bool top_on() {
+  const char* v = std::getenv("DPF_EXPAND_TOP");
+  return !(v && v[0] == '0');
+}
+struct TopScratch {
+  void* mem = nullptr;
+  hipStream_t s = nullptr;
+  ~TopScratch() {
+    if (mem) (void)hipFreeAsync(mem, s);
+  }
+};
+// Returns the error of a failed launch, else kOk (p rewritten when the pass ran).
+int expand_top(ExpandParams& p, hipStream_t s, TopScratch& scratch) {
+  const int64_t starts = p.num_items >> p.k0;
+  // Few start seeds (full-domain calls and their shards): with many starts
+  // every item's walk is short and a workgroup per start would idle.
+  if (!top_on() || p.k0 < 8 || starts > num_cus() || p.num_items < 4 * (int64_t)num_cus())
+    return kOk;
+  // Workgroups: one per subtree at depth t under each start, at least one
+  // per CU; D = k0 - t levels breadth-first (1..kSmallMaxD).
+  int t = 0;
+  while ((starts << t) < num_cus() && t < p.k0 - 1) ++t;
+  if (p.k0 - t > kSmallMaxD) t = p.k0 - kSmallMaxD;
+  const int D = p.k0 - t;
+  if (D < 1 || (starts << t) > INT32_MAX) return kOk;
+  static const bool pool_kept = [] {
+    int dev = 0;
+    hipMemPool_t pool;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetDefaultMemPool(&pool, dev) != hipSuccess)
+      return false;
+    uint64_t keep = UINT64_MAX;
+    return hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) == hipSuccess;
+  }();
+  (void)pool_kept;
+  const size_t items = (size_t)p.num_items;
+  void* mem = nullptr;
+  HIP_TRY(hipMallocAsync(&mem, items * (sizeof(dpf_block) + 1), s));
+  scratch.mem = mem;
+  scratch.s = s;
+  SeedLeaf leaf{static_cast<dpf_block*>(mem),
+                static_cast<uint8_t*>(mem) + items * sizeof(dpf_block)};
+  ExpandParams q = p;
+  q.k0 = t;
+  q.S = D;
+  q.num_levels = p.k0;
+  q.num_items = starts << t;
+  q.clock = nullptr;
+  hipLaunchKernelGGL((expand_small_kernel<SeedLeaf>), dim3((unsigned)q.num_items), dim3(kBlock), 0,
+                     s, q, leaf);
+  HIP_TRY(hipGetLastError());
+  // The octet kernel starts at the item roots: k0 = 0, correction words from
+  // level k0 on.
+  p.seeds_in = leaf.seeds;
+  p.ctrl_in = leaf.ctrl;
+  p.cw_seed += p.k0;
+  p.cw_left += p.k0;
+  p.cw_right += p.k0;
+  p.num_levels = p.S;
+  p.k0 = 0;
+  return kOk;
+}
+
 // The octet kernel takes integer leaves filling whole blocks whenever the
 // subtrees have >= 8 leaves (DPF_EXPAND_NO_OCTET=1 forces expand_kernel).
 template <int BITS, bool XOR>
-bool launch_octet(const ExpandParams& p, const dpf_block* vcw, int E, int party, int store_bytes,
-                  hipStream_t s) {
+bool launch_octet(const ExpandParams& p0, const dpf_block* vcw, int E, int party, int store_bytes,
+                  hipStream_t s, int* st) {
   const char* off = getenv("DPF_EXPAND_NO_OCTET");
-  if ((off && off[0] == '1') || store_bytes != 16 || p.S < 3) return false;
-  note_expand<FastIntLeaf<BITS, XOR>>(p, true);
+  if ((off && off[0] == '1') || store_bytes != 16 || p0.S < 3) return false;
+  note_expand<FastIntLeaf<BITS, XOR>>(p0, true);
+  ExpandParams p = p0;
+  TopScratch top;
+  if ((*st = expand_top(p, s, top)) != kOk) return true;
   const int blk = block_for(p.num_items);
   hipLaunchKernelGGL((expand_octet_kernel<FastIntLeaf<BITS, XOR>>), dim3(grid_for(p.num_items, blk)),
                      dim3(blk), 0, s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
@@ -857,8 +948,10 @@ int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf
     HIP_TRY(hipGetLastError());
     return kOk;
   }
-  if (d->kind[0] == DPF_LEAF_XOR ? launch_octet<BITS, true>(p, vcw, E, party, store_bytes, s)
-                                 : launch_octet<BITS, false>(p, vcw, E, party, store_bytes, s)) {
+  int st = kOk;
+  if (d->kind[0] == DPF_LEAF_XOR ? launch_octet<BITS, true>(p, vcw, E, party, store_bytes, s, &st)
+                                 : launch_octet<BITS, false>(p, vcw, E, party, store_bytes, s, &st)) {
+    if (st != kOk) return st;
     HIP_TRY(hipGetLastError());
     return kOk;
   }
@@ -2034,6 +2127,8 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       }
       if (p.S >= 3 && !(off_env && off_env[0] == '1')) {
         note_expand<SwarLeaf>(p, true);
+        TopScratch top;
+        if (int st = expand_top(p, s, top)) return st;
         const int blk = block_for(p.num_items);
         hipLaunchKernelGGL((expand_octet_kernel<SwarLeaf>), dim3(grid_for(p.num_items, blk)),
                            dim3(blk), 0, s, p, w);
@@ -2065,6 +2160,8 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       if (p.S >= 3 && !(off && off[0] == '1')) {
         // Octet form (the half's four leaves hashed as two ILP4 groups).
         note_expand<Mod32Leaf<2>>(p, true);
+        TopScratch top;
+        if (int st = expand_top(p, s, top)) return st;
         const int blk = block_for(p.num_items);
         hipLaunchKernelGGL((expand_octet_kernel<Mod32Leaf<2>>), dim3(grid_for(p.num_items, blk)),
                            dim3(blk), 0, s, p, m);

@@ -36,7 +36,8 @@ struct HHLevelArgs {
   const uint8_t* ctrl_in;    // NULL: control bit in bit 0 of the seed
   int64_t in_stride;
   const int32_t* parent;
-  const int32_t* save_index;  // NULL: no partial evaluations stored
+  int save;                   // 1: store each start node as the key's partial evaluation
+  const int32_t* save_index;  // NULL (with save): start node u at index u
   dpf_block* seeds_out;
   uint8_t* ctrl_out;
   int64_t out_stride;

@@ -148,6 +148,11 @@ class DeviceBatchContext {
   // Allocates exactly `bytes` into *p (*p must be null); false on failure.
   bool TryAlloc(void** p, size_t* cap, size_t bytes);
   void Release(void** p, size_t* cap);
+  // Page-locked image of a call's start-node tables (and output offsets),
+  // sent with one asynchronous H2D: StageTables waits for the previous
+  // call's copy and makes room for `bytes`; TablesSent marks the copy.
+  Status StageTables(size_t bytes);
+  Status TablesSent(void* stream);
   // Free and total device memory as this context sees it (DPF_BATCH_ALLOC_LIMIT
   // replaces the device's figures with the limit, as a test hook).
   void MemInfo(size_t* free_bytes, size_t* total_bytes) const;
@@ -191,7 +196,12 @@ class DeviceBatchContext {
   size_t device_bytes_ = 0;  // sum of the caps below and above
   CacheEvents events_;
   int fail_next_ = 0, fail_skip_ = 0;
-  // Per-call scratch: start-node tables, sums workspace, staging output.
+  void* pinned_tables_ = nullptr;
+  size_t pinned_tables_cap_ = 0;
+  void* tables_event_ = nullptr;
+  bool tables_pending_ = false;
+  // Per-call scratch: start-node tables (parent_: the device copy of the
+  // whole table image), sums workspace, staging output.
   void* parent_ = nullptr;
   void* path_ = nullptr;
   void* save_ = nullptr;

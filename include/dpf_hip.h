@@ -308,7 +308,7 @@ int dpf_hip_sum_shares_u64(int64_t num_keys, int64_t row_len, int bits, int xor_
  *          with key k's correction words cw_first + j (rows of cw_stride);
  *          after save_after steps (-1 = never) the node is stored at
  *          seeds_out/control_out[k*out_stride + save_index[u]] when
- *          save_index[u] >= 0;
+ *          save_index[u] >= 0 (save_index == NULL: at index u);
  *   expand expand_levels (<= dpf_hip_prefix_batch_max_expand) full levels
  *          below it (correction words cw_first + walk_levels + d), hash
  *          every leaf, convert it and keep its first elements_per_leaf

@@ -11,6 +11,7 @@
 // Run by tests/test_cpp_api_gpu.py; built by build_native.build_tools.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <string>
 #include <vector>
@@ -21,6 +22,8 @@
 #include "dpf/tuple.h"
 #include "dpf/xor_wrapper.h"
 #include "dpf_hip.h"
+// The library's internal D2H helpers (CopyToHostSink), for the grow-failure test.
+#include "../../distributed_point_functions_amd/csrc/host/host_util.h"
 
 namespace dpf = distributed_point_functions;
 using dpf::DistributedPointFunction;
@@ -100,6 +103,54 @@ void FullDomain(const std::string& name, int log) {
     if (!(at0[j] == a[static_cast<size_t>(pts[j])]))
       Fail(name + ": EvaluateAt != EvaluateUntil at point " + std::to_string(j));
   g_checks += 2;
+}
+
+// EvaluateAt<T> with a 4-32 MiB result (the overlapped-growth range of
+// CopyToHostSink; run with DPF_OVERLAP_GROW=0 and 1 by test_cpp_api_gpu.py):
+// every point's value equals the full-domain output's.
+template <typename T>
+void LargeEvaluateAt(const std::string& name, int log, int64_t npts) {
+  DpfParameters p;
+  p.set_log_domain_size(log);
+  *p.mutable_value_type() = dpf::ToValueType<T>();
+  auto f = Must(DistributedPointFunction::Create(p), "Create");
+  if (!f->template RegisterValueType<T>().ok()) Fail("RegisterValueType " + name);
+  std::mt19937_64 rng(log * 104729 + npts);
+  const uint128 domain = uint128{1} << log;
+  auto keys = Must(f->GenerateKeys(dpf::MakeUint128(rng(), rng()) % domain, Beta<T>()), "keys");
+  EvaluationContext c0 = Must(f->CreateEvaluationContext(keys.first), "ctx");
+  std::vector<T> full = Must(f->template EvaluateUntil<T>(0, {}, c0), "EvaluateUntil " + name);
+  std::vector<uint128> pts(static_cast<size_t>(npts));
+  for (auto& x : pts) x = dpf::MakeUint128(rng(), rng()) % domain;
+  std::vector<T> at = Must(f->template EvaluateAt<T>(keys.first, 0, pts), "EvaluateAt " + name);
+  if (at.size() != pts.size()) Fail(name + ": EvaluateAt size");
+  for (size_t j = 0; j < pts.size(); ++j)
+    if (!(at[j] == full[static_cast<size_t>(pts[j])]))
+      Fail(name + ": large EvaluateAt != EvaluateUntil at " + std::to_string(j));
+  ++g_checks;
+}
+
+// A result sink whose growth throws (no memory for the result) makes the
+// device-to-host copy fail with an error, on the overlapped path (grow on a
+// helper thread, 4-32 MiB) and on the chunk-by-chunk path -- never terminate.
+void GrowFailureIsAnError() {
+  const size_t bytes = size_t{8} << 20;
+  void* dev = nullptr;
+  if (dpf_hip_alloc(&dev, bytes) != 0 || dpf_hip_memset(dev, 0x5A, bytes, nullptr) != 0)
+    Fail("device buffer");
+  std::vector<uint8_t> host(bytes);
+  dpf::dpf_internal::HostSink sink;
+  sink.reserve = [&](size_t) -> void* { return host.data(); };
+  sink.grow = [](size_t) { throw std::bad_alloc(); };
+  sink.chunk = [&](const uint8_t* src, size_t off, size_t len) { std::memcpy(host.data() + off, src, len); };
+  for (const char* mode : {"1", "0"}) {
+    setenv("DPF_OVERLAP_GROW", mode, 1);
+    const int rc = dpf::dpf_internal::CopyToHostSink(sink, host.data(), dev, bytes, nullptr);
+    if (rc == 0) Fail(std::string("grow failure not reported, DPF_OVERLAP_GROW=") + mode);
+    ++g_checks;
+  }
+  unsetenv("DPF_OVERLAP_GROW");
+  dpf_hip_free(dev);
 }
 
 // Hierarchical evaluation (distributed_point_function_test.cc:932-1030):
@@ -240,6 +291,12 @@ int main() {
   FullDomain<dpf::Tuple<uint32_t, uint64_t>>("Tuple<uint32_t, uint64_t>", 23);
   FullDomain<dpf::Tuple<ModN32, ModN32>>("Tuple<IntModN32 x2>", 22);
   FullDomain<uint64_t>("uint64_t", 26);
+  // EvaluateAt results of 8, 16, 20 and 16 MiB.
+  LargeEvaluateAt<uint64_t>("uint64_t", 24, int64_t{1} << 20);
+  LargeEvaluateAt<uint128>("uint128", 22, int64_t{1} << 20);
+  LargeEvaluateAt<U32x5>("Tuple<uint32_t x5>", 20, int64_t{1} << 20);
+  LargeEvaluateAt<dpf::Tuple<ModN32, ModN32>>("Tuple<IntModN32 x2>", 22, int64_t{1} << 21);
+  GrowFailureIsAnError();
   Hierarchical();
   DeviceRetryAfterSmallBuffer();
   for (int log : {3, 16, 64}) {

@@ -341,9 +341,9 @@ def test_cache_evicted_after_in_place_gather(monkeypatch):
     the partial evaluations and rebuilds it."""
     monkeypatch.setenv("DPF_BATCH_CACHE_IN_PLACE", "1")
     levels, plan = HH5
-    # Six per-call buffers precede the gather (parent/path/save tables, the
-    # next partial evaluations' seeds and control bits, the cache slots).
-    arm = lambda i, c: c.fail_next_allocations_for_testing(1, skip=6) if i == 2 else None
+    # Four per-call buffers precede the gather (the start-node table image,
+    # the next partial evaluations' seeds and control bits, the cache slots).
+    arm = lambda i, c: c.fail_next_allocations_for_testing(1, skip=4) if i == 2 else None
     bctx, failed, _ = _pressure_run(levels, plan, 17, True, seed=93, arm=arm)
     ev = bctx.cache_events
     assert failed == [] and ev["evicted_cache"] == 1 and ev["evicted_spare"] == 0, ev

@@ -13,8 +13,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "distributed_point_functions_amd", "lib", "dpf_api_test")
 
 
-def test_cpp_template_api():
+@pytest.mark.parametrize("overlap_grow", ["1", "0"])
+def test_cpp_template_api(overlap_grow):
+    # DPF_OVERLAP_GROW: 4-32 MiB results value-initialised on a helper thread
+    # during the DMA (default) or chunk by chunk (host_util.h CopyToHostSink);
+    # the typed EvaluateUntil / EvaluateAt results of that size (VectorSink and
+    # the tuple / IntModN unpacking sink) must be identical either way.
     assert os.path.exists(BIN), "build first: python -m distributed_point_functions_amd.build_native"
-    r = subprocess.run([BIN], capture_output=True, text=True, timeout=240)
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, DPF_OVERLAP_GROW=overlap_grow))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ALL OK" in r.stdout
