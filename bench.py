@@ -1104,7 +1104,7 @@ def main_heavy_hitters(args):
             "verified": ("two-server reconstruction == plaintext prefix histogram at every level"
                          if verified else False),
             "true_top_k_recall": len(true_top & set(final)) / max(len(true_top), 1),
-            **aes_rooflines(achieved, "hh_level_kernel (cached levels) + batch_level_kernel<Mod32V, 2, true> (level 0)",
+            **aes_rooflines(achieved, "hh_keys_kernel (cached levels) + batch_level_kernel<Mod32V, 2, true> (level 0)",
                             traffic=tr[0] if tr else None, traffic_unit="bytes per pass",
                             traffic_source=tr[1] if tr else None, pmc=tr[2] if tr else None,
                             launch_ms_per_pass=kern_ms_max, algorithmic_aes_per_pass=aes_rank),

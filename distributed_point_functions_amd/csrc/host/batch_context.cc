@@ -329,14 +329,20 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   const int64_t P = static_cast<int64_t>(prefixes.size());
   // Host buffers are recycled across calls: first touches of fresh pages cost
   // more than the bookkeeping itself at 1 M prefixes per level (config 5a).
+  // Not cleared first: DedupTreeIndices overwrites every element, so vectors
+  // kept from an earlier call of about this size value-initialise nothing
+  // (clearing them had cost a 1 M-prefix level ~3.8 ms of single-threaded
+  // zeroing, r16 DPF_BATCH_HOST_TIMING).
   std::vector<uint128> tree_indices = std::move(ctx.spare_prefixes_);
-  tree_indices.clear();
   static thread_local std::vector<std::pair<int64_t, int>> tl_prefix_map;
   std::vector<std::pair<int64_t, int>>& prefix_map = tl_prefix_map;
-  prefix_map.clear();
-  if (P > 0)
+  if (P > 0) {
     dpf_internal::DedupTreeIndices(prefixes, prev_log - hierarchy_to_tree()[prev], &tree_indices,
                                    &prefix_map);
+  } else {
+    tree_indices.clear();
+    prefix_map.clear();
+  }
 
   clk.mark(0);
   // Where each tree index starts: a stored partial evaluation or the root
@@ -344,7 +350,8 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   const int Dh = hierarchy_to_tree()[hierarchy_level];
   int Dprev = 0, start_level = 0;
   bool from_root = true;
-  std::vector<int32_t> parent_of;
+  static thread_local std::vector<int32_t> tl_parent_of;   // recycled: no per-call zeroing
+  std::vector<int32_t>& parent_of = tl_parent_of;
   if (P == 0) {
     tree_indices.assign(1, 0);  // the root, expanded to depth Dh
   } else {
@@ -355,7 +362,18 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
       start_level = hierarchy_to_tree()[ctx.partial_evaluations_level_];
       from_root = false;
       const int shift = Dprev - start_level;
-      const bool sorted = std::is_sorted(q.begin(), q.end());
+      // Sortedness of the stored prefixes, checked in chunks on host threads.
+      const int64_t nq = static_cast<int64_t>(q.size());
+      const int qchunks = dpf_internal::NumChunks(nq);
+      std::vector<char> q_ok(qchunks, 1);
+      dpf_internal::ParallelChunks(nq, qchunks, [&](int c, int64_t lo, int64_t hi) {
+        for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
+          if (q[j] < q[j - 1]) {
+            q_ok[c] = 0;
+            return;
+          }
+      });
+      const bool sorted = std::all_of(q_ok.begin(), q_ok.end(), [](char x) { return x != 0; });
       std::unordered_map<uint128, int32_t, U128Hash> pos;
       if (!sorted) {
         pos.reserve(q.size() * 2);

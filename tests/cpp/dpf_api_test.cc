@@ -141,8 +141,13 @@ void GrowFailureIsAnError() {
   std::vector<uint8_t> host(bytes);
   dpf::dpf_internal::HostSink sink;
   sink.reserve = [&](size_t) -> void* { return host.data(); };
+  // As VectorSink: grow() sizes the result up front on the overlapped path,
+  // and chunk() grows it chunk by chunk otherwise.
   sink.grow = [](size_t) { throw std::bad_alloc(); };
-  sink.chunk = [&](const uint8_t* src, size_t off, size_t len) { std::memcpy(host.data() + off, src, len); };
+  sink.chunk = [&](const uint8_t* src, size_t off, size_t len) {
+    sink.grow(off + len);
+    std::memcpy(host.data() + off, src, len);
+  };
   for (const char* mode : {"1", "0"}) {
     setenv("DPF_OVERLAP_GROW", mode, 1);
     const int rc = dpf::dpf_internal::CopyToHostSink(sink, host.data(), dev, bytes, nullptr);
