@@ -36,6 +36,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <vector>
+
 #include "../../../include/dpf_hip.h"
 #include "dpf_device.h"
 #include "dpf_runtime.h"
@@ -798,6 +800,37 @@ int dpf_hip_eval_prefix_batch_cached_slots(
       0, stream);
 }
 
+namespace {
+// DPF_HIP_CHECK_SLOTS=1 (read per call): the slot table's contract
+// (include/dpf_hip.h) checked on the host before the launch -- every slot
+// below leaf_stride, no slot written twice, and a slot some start node reads
+// written only as a leaf of that node and only if no other node reads it.
+// A table breaking it would overwrite start seeds before they are read, or
+// write out of bounds.  Costs two D2H copies; a debugging aid.
+int check_slot_table(int64_t num_starts, int expand_levels, const int32_t* parent,
+                     const int32_t* leaf_slot, int64_t leaf_stride) {
+  const int64_t U = num_starts, n = U << expand_levels;
+  std::vector<int32_t> par(U), slot(n);
+  HIP_TRY(hipMemcpy(par.data(), parent, U * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(slot.data(), leaf_slot, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int64_t> reader(leaf_stride, -1);   // start node reading each slot (-2: several)
+  for (int64_t u = 0; u < U; ++u) {
+    if (par[u] < 0 || par[u] >= leaf_stride) return fail(kInvalidArgument, "slot table: parent out of range");
+    reader[par[u]] = reader[par[u]] == -1 ? u : -2;
+  }
+  std::vector<char> written(leaf_stride, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t v = slot[i];
+    if (v < 0 || v >= leaf_stride) return fail(kInvalidArgument, "slot table: slot out of range");
+    if (written[v]++) return fail(kInvalidArgument, "slot table: slot written twice");
+    const int64_t r = reader[v];
+    if (r == -2 || (r >= 0 && r != (i >> expand_levels)))
+      return fail(kInvalidArgument, "slot table: a slot another start node reads is overwritten");
+  }
+  return kOk;
+}
+}  // namespace
+
 int dpf_hip_eval_prefix_batch_layout(
     int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
     int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,
@@ -890,6 +923,12 @@ int dpf_hip_eval_prefix_batch_layout(
       p.leaf_seeds = leaf_cache;
       p.leaf_stride = leaf_stride;
       p.leaf_slot = leaf_slot;
+      const char* chk = getenv("DPF_HIP_CHECK_SLOTS");
+      if (leaf_slot && seeds_in && chk && chk[0] == '1') {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (int e = check_slot_table(num_starts, expand_levels, parent, leaf_slot, leaf_stride))
+          return e;
+      }
     }
     p.rkl = expand_key(key_left);
     p.rkr = expand_key(key_right);

@@ -239,8 +239,10 @@ void hh_level_kernel(HHParams p) {
       Block4 s = s_next;
       const uint32_t c_in = c_next;
 #else
-      Block4 s = load_block(p.seeds_in + k * p.in_stride + par);
-      const uint32_t c_in = p.ctrl_in ? p.ctrl_in[k * p.in_stride + par] : 0u;
+      // Padding lanes (u clamped to U - 1) read nothing: that node's own
+      // lane may be rewriting the slot in place.
+      Block4 s = valid ? load_block(p.seeds_in + k * p.in_stride + par) : Block4{0, 0, 0, 0};
+      const uint32_t c_in = p.ctrl_in && valid ? p.ctrl_in[k * p.in_stride + par] : 0u;
 #endif
       uint32_t t;
       if (p.ctrl_in) {
@@ -461,11 +463,13 @@ struct HHKeysLds {
 #endif
 };
 
-// DPF_HH_NT=1: the streamed start seeds, cache leaves and partial
-// evaluations bypass L2 allocation (non-temporal), leaving L2 to the waves'
-// key tables (A/B variant).
+// DPF_HH_NT=1 (default): the streamed start seeds, cache leaves and partial
+// evaluations are non-temporal (they are not read again within the call),
+// leaving L2 to the waves' key tables: 2^20-client pass 19.03 / 19.23 /
+// 19.25 vs 19.16 / 19.37 / 19.34 s with temporal accesses, three same-box
+// pairs (profiles/r16/hh_nt_ab.txt).
 #ifndef DPF_HH_NT
-#define DPF_HH_NT 0
+#define DPF_HH_NT 1
 #endif
 __device__ __forceinline__ Block4 stream_load(const dpf_block* p) {
 #if DPF_HH_NT

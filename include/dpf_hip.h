@@ -371,7 +371,8 @@ int dpf_hip_eval_prefix_batch_cached(
  * before it has been read -- no gather of the start seeds and no second
  * cache buffer (the heavy-hitters steady state at 2^20
  * clients, where a 64 GiB spare does not fit).  leaf_slot == NULL: exactly
- * dpf_hip_eval_prefix_batch_cached. */
+ * dpf_hip_eval_prefix_batch_cached.  DPF_HIP_CHECK_SLOTS=1 checks the table
+ * against this contract on the host first (INVALID_ARGUMENT if broken). */
 int dpf_hip_eval_prefix_batch_cached_slots(
     int64_t num_keys, int64_t num_starts, int walk_levels, int save_after, int expand_levels,
     int cw_first, int cw_stride, const dpf_block* key_seed, const uint8_t* party,

@@ -456,3 +456,59 @@ def test_hh_keys_kernel_key_groups(n_keys, mode, monkeypatch):
         monkeypatch.setenv("DPF_BATCH_CACHE_MODE", mode)
     levels, plan = HH5
     _pressure_run(levels, plan, n_keys, True, seed=n_keys + 3)
+
+
+def test_permuted_cache_slot_tables_pass_the_contract_check(monkeypatch):
+    """DPF_HIP_CHECK_SLOTS=1: every slot table the context builds for an
+    in-place rewrite satisfies the contract of
+    dpf_hip_eval_prefix_batch_cached_slots (checked on the host before each
+    launch) -- in both table layouts."""
+    monkeypatch.setenv("DPF_HIP_CHECK_SLOTS", "1")
+    monkeypatch.setenv("DPF_BATCH_CACHE_MODE", "permute")
+    levels, plan = HH5
+    bctx, failed, _ = _pressure_run(levels, plan, 40, True, seed=98)
+    assert failed == [] and bctx.cache_events["permuted"] >= 1
+    monkeypatch.setenv("DPF_BATCH_KEY_MAJOR", "1")
+    bctx, failed, _ = _pressure_run(levels, plan, 40, True, seed=98)
+    assert failed == [] and bctx.cache_events["permuted"] >= 1
+
+
+@pytest.mark.parametrize("bad", ["out_of_range", "twice", "overwrites_other_reader"])
+def test_broken_slot_table_is_rejected(bad, monkeypatch):
+    """A slot table breaking the contract is INVALID_ARGUMENT under
+    DPF_HIP_CHECK_SLOTS=1, before anything is launched."""
+    import ctypes
+    import torch
+    from distributed_point_functions_amd import hip_abi as H
+    monkeypatch.setenv("DPF_HIP_CHECK_SLOTS", "1")
+    L = H.load(require_gpu=True)
+    K, U, E, stride = 4, 2, 2, 8
+    dev = "cuda"
+    blocks = lambda n: torch.zeros((n, 2), dtype=torch.int64, device=dev)
+    key_seed, cw_seed, vcw = blocks(K), blocks(K * 2), blocks(K * 2)
+    party = torch.zeros(K, dtype=torch.uint8, device=dev)
+    cw_l = torch.zeros(K * 2, dtype=torch.uint8, device=dev)
+    cw_r = torch.zeros(K * 2, dtype=torch.uint8, device=dev)
+    cache = blocks(K * stride)
+    parent = torch.tensor([0, 1], dtype=torch.int32, device=dev)
+    slots = {"out_of_range": [0, 2, 3, 8, 1, 4, 5, 6],
+             "twice": [0, 2, 3, 4, 1, 4, 5, 6],
+             "overwrites_other_reader": [0, 1, 3, 4, 2, 5, 6, 7]}[bad]
+    leaf_slot = torch.tensor(slots, dtype=torch.int32, device=dev)
+    out = torch.zeros(K * (U << E) * 8, dtype=torch.uint8, device=dev)
+    desc = H.value_desc([(H.LEAF_INT, 64, 0)], True, 2, 1)
+    kl, kr, kv = H.aes_key(1), H.aes_key(2), H.aes_key(3)
+    P, I64, I = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    f = L.dpf_hip_eval_prefix_batch_layout
+    f.argtypes = [I64, I64, I, I, I, I, I, P, P, P, P, I64, P, P, P, P, P, I64, P, P, P, P, P, P,
+                  P, I, P, I, P, P, P, I64, P, I, P]
+    for index_major in (0, 1):
+        rc = f(K, U, 0, -1, E, 0, 2, key_seed.data_ptr(), party.data_ptr(), cache.data_ptr(), None,
+               stride, parent.data_ptr(), None, None, None, None, 0, cw_seed.data_ptr(),
+               cw_l.data_ptr(), cw_r.data_ptr(), ctypes.byref(kl), ctypes.byref(kr),
+               ctypes.byref(kv), ctypes.byref(desc), 2, vcw.data_ptr(), 0, None, out.data_ptr(),
+               cache.data_ptr(), stride, leaf_slot.data_ptr(), index_major,
+               H._stream(None))
+        assert rc == 3, (bad, rc)
+        assert "slot table" in L.dpf_hip_last_error().decode()
+    torch.cuda.synchronize()
