@@ -868,6 +868,16 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilToDevice(
   return n;
 }
 
+void DistributedPointFunction::ReleaseScratch() {
+  // The old scratch's destructors wait for the events of its images and free
+  // its buffers (long-lived objects kept their largest call's).
+  std::unique_ptr<dpf_internal::DeviceScratch> fresh(new dpf_internal::DeviceScratch());
+  {
+    std::lock_guard<std::recursive_mutex> lock(scratch_->mu);
+  }
+  scratch_.swap(fresh);
+}
+
 StatusOr<int64_t> DistributedPointFunction::EvaluateShardToDevice(
     int hierarchy_level, int64_t shard, int64_t num_shards, EvaluationContext& ctx,
     void* device_out, int64_t capacity_bytes, void* stream) const {

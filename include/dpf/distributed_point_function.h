@@ -296,6 +296,13 @@ class DistributedPointFunction {
                                                       const KeyBatch& host_keys, int64_t k,
                                                       void* stream) const;
 
+  // Gives back the per-object host and device scratch the evaluation calls
+  // keep between calls (page-locked argument images, staging, device buffers,
+  // the prefix dedup's vectors): hundreds of MB after one huge hierarchical
+  // call.  Waits for work in flight that reads them; the next call
+  // reallocates.  Must not run concurrently with a call on this object.
+  void ReleaseScratch();
+
   // Group sum of `num_shares` packed output vectors of `count` elements each
   // (host memory), e.g. per-GPU partial sums after an all-gather.
   StatusOr<std::vector<uint8_t>> SumPackedShares(int hierarchy_level, const uint8_t* shares,

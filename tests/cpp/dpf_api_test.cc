@@ -120,6 +120,7 @@ void LargeEvaluateAt(const std::string& name, int log, int64_t npts) {
   auto keys = Must(f->GenerateKeys(dpf::MakeUint128(rng(), rng()) % domain, Beta<T>()), "keys");
   EvaluationContext c0 = Must(f->CreateEvaluationContext(keys.first), "ctx");
   std::vector<T> full = Must(f->template EvaluateUntil<T>(0, {}, c0), "EvaluateUntil " + name);
+  f->ReleaseScratch();   // the next call reallocates what it needs
   std::vector<uint128> pts(static_cast<size_t>(npts));
   for (auto& x : pts) x = dpf::MakeUint128(rng(), rng()) % domain;
   std::vector<T> at = Must(f->template EvaluateAt<T>(keys.first, 0, pts), "EvaluateAt " + name);
