@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarises one rocprofv3 collection directory (trace/ with --kernel-trace
---stats, and p*/ PMC passes, as written by profiles/profile.sh or
-tools/hyb_profile.sh) for one kernel into the profiles/<tag>_summary.json
+--stats, and p*/ PMC passes, as written by tools/profile_workload.sh or
+profiles/profile.sh) for one kernel into the profiles/<tag>_summary.json
 format: per-launch counter averages, the sustained clock, LDS-pipe busy
 fraction, VALU / LDS instructions per AES block and HBM write bytes (WRITE_SIZE
 is in KiB on gfx950, MI355X_MICROARCH.md; GRBM_GUI_ACTIVE sums the 8 XCDs).
