@@ -614,7 +614,9 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     total = outputs_per_rank * world * args.steps
     n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    ghz = clock["clock_ghz"]
+    # 0 workgroups stamped: the launches ran a kernel without the probe
+    # (expand_small_kernel, latency mode: config 1) -- no clock, not 0 GHz.
+    ghz = clock["clock_ghz"] if clock["workgroups"] else None
     if rank == 0:
         # The committed rocprof summaries are of the one-GPU lines.
         tr = (profiled_traffic(kernel_name(args, bits), outputs_per_rank, workload=workload_tag(args))
@@ -658,9 +660,10 @@ def main():
                             sustained_clock_ghz_per_rank=clocks,
                             clk_per_aes_per_cu=(kern_ms * 1e-3 * ghz * 1e9 * n_cus / aes_per_launch
                                                 if ghz else None),
-                            clock_source="s_memtime/s_memrealtime stamps of every workgroup of the "
-                                         f"timed launches ({clock['workgroups']} workgroups, "
-                                         f"{clock['mean_workgroup_ms']:.3f} ms each on average)",
+                            clock_source=("s_memtime/s_memrealtime stamps of every workgroup of the "
+                                          f"timed launches ({clock['workgroups']} workgroups, "
+                                          f"{clock['mean_workgroup_ms']:.3f} ms each on average)"
+                                          if ghz else "none: the timed kernel carries no clock probe"),
                             cus=n_cus),
             # Fixed per-step cost: wall time per step beyond the launch's own
             # HIP-event time (host validation, the packed image, launch gaps).

@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
 """Prints DESIGN.md section 5's all-workload table from a round's bench lines
-(profiles/<tag>_*_bench.json, written by tools/round_evidence.sh), so the table
-quotes exactly the committed evidence.
+(profiles/<tag>/bench_<tag>_<workload>.json and, for config 2,
+profiles/<tag>_bench.json -- copied from tools/round_evidence.sh's gpurun_out/;
+rounds up to r15: profiles/<tag>_<workload>_bench.json), so the table quotes
+exactly the committed evidence.  The last column is the sustained clock the
+line measured inside its own launches (in-kernel stamps, r16) or, for older
+lines, the clock of the same lease's profile.
 
-  python tools/workload_table.py r14
+  python tools/workload_table.py r16
 """
 import json
 import os
@@ -46,15 +50,22 @@ def cpu(d):
     return f"{v:.0f} {u}"
 
 
+def bench_path(tag: str, suffix: str) -> str:
+    for p in ((f"{tag}_bench.json",) if suffix == "full_domain" else ()) + (
+            os.path.join(tag, f"bench_{tag}_{suffix}.json"), f"{tag}_{suffix}_bench.json"):
+        if os.path.exists(os.path.join(ROOT, "profiles", p)):
+            return os.path.join(ROOT, "profiles", p)
+    raise FileNotFoundError(f"no {tag} bench line for {suffix} under profiles/")
+
+
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r15"
-    print("| workload | result | G AES/s | VALU roofline | clock (GHz, profile) | CPU baseline (16 host threads) |")
+    print("| workload | result | G AES/s | VALU roofline | clock (GHz) | CPU baseline (16 host threads) |")
     print("|---|---|---|---|---|---|")
     for suffix, label, fmt in ROWS:
-        path = os.path.join(ROOT, "profiles", f"{tag}_{suffix}_bench.json")
-        d = json.loads(open(path).read().strip().splitlines()[-1])
+        d = json.loads(open(bench_path(tag, suffix)).read().strip().splitlines()[-1])
         r = d.get("roofline", {})
-        ghz = (r.get("pmc") or {}).get("sustained_clock_ghz")
+        ghz = r.get("sustained_clock_ghz") or (r.get("pmc") or {}).get("sustained_clock_ghz")
         print(f"| {label} | {fmt(d)} | {r.get('achieved', 0):.1f} | {r.get('frac', 0):.3f} | "
               f"{ghz:.2f} | {cpu(d)} |" if ghz else
               f"| {label} | {fmt(d)} | {r.get('achieved', 0):.1f} | {r.get('frac', 0):.3f} | — | {cpu(d)} |")
