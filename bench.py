@@ -591,7 +591,8 @@ def main():
     H.clock_probe(False)
     if group_up(dist):
         dist.barrier()
-    kern_ms = float(np.mean([a.elapsed_ms(b) for a, b in evs]))
+    per_step_ms = [a.elapsed_ms(b) for a, b in evs]
+    kern_ms = float(np.mean(per_step_ms))
     elapsed = S.max_over_ranks(t1 - t0, device=coll)
     kern_ms_max = S.max_over_ranks(kern_ms, device=coll)
     ginfo = S.group_info(kern_ms, device=coll)
@@ -669,7 +670,11 @@ def main():
             # HIP-event time (host validation, the packed image, launch gaps).
             "step_overhead": {"ms_per_step": ms_per_step, "launch_ms": kern_ms_max,
                               "overhead_ms": ms_per_step - kern_ms_max,
-                              "overhead_frac": (ms_per_step - kern_ms_max) / ms_per_step},
+                              "overhead_frac": (ms_per_step - kern_ms_max) / ms_per_step,
+                              # rank 0's launches in order: a clock still ramping
+                              # shows as first >> last.
+                              "launch_ms_first": per_step_ms[0], "launch_ms_last": per_step_ms[-1],
+                              "launch_ms_min": min(per_step_ms), "launch_ms_max": max(per_step_ms)},
             "process_group": ginfo,
             "roofline_hbm": {"bound": "hbm",
                              "achieved": bytes_per_launch / (kern_ms_max * 1e-3) / 1e9,
