@@ -210,6 +210,7 @@ void DeviceBatchContext::Reset(bool release_expansion_cache) {
   previous_hierarchy_level_ = -1;
   partial_evaluations_level_ = -1;
   partial_prefixes_.clear();
+  partial_sorted_ = false;
   leaf_level_ = -1;
   if (release_expansion_cache) {
     (void)dpf_hip_stream_sync(nullptr);  // work still reading the cache
@@ -336,9 +337,10 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   std::vector<uint128> tree_indices = std::move(ctx.spare_prefixes_);
   static thread_local std::vector<std::pair<int64_t, int>> tl_prefix_map;
   std::vector<std::pair<int64_t, int>>& prefix_map = tl_prefix_map;
+  bool indices_ascending = false;   // tree_indices strictly ascending
   if (P > 0) {
     dpf_internal::DedupTreeIndices(prefixes, prev_log - hierarchy_to_tree()[prev], &tree_indices,
-                                   &prefix_map);
+                                   &prefix_map, &indices_ascending);
   } else {
     tree_indices.clear();
     prefix_map.clear();
@@ -362,18 +364,23 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
       start_level = hierarchy_to_tree()[ctx.partial_evaluations_level_];
       from_root = false;
       const int shift = Dprev - start_level;
-      // Sortedness of the stored prefixes, checked in chunks on host threads.
-      const int64_t nq = static_cast<int64_t>(q.size());
-      const int qchunks = dpf_internal::NumChunks(nq);
-      std::vector<char> q_ok(qchunks, 1);
-      dpf_internal::ParallelChunks(nq, qchunks, [&](int c, int64_t lo, int64_t hi) {
-        for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
-          if (q[j] < q[j - 1]) {
-            q_ok[c] = 0;
-            return;
-          }
-      });
-      const bool sorted = std::all_of(q_ok.begin(), q_ok.end(), [](char x) { return x != 0; });
+      // Sortedness of the stored prefixes: known when they came from an
+      // ascending dedup (the hierarchical case), else checked in chunks on
+      // host threads.
+      bool sorted = ctx.partial_sorted_;
+      if (!sorted) {
+        const int64_t nq = static_cast<int64_t>(q.size());
+        const int qchunks = dpf_internal::NumChunks(nq);
+        std::vector<char> q_ok(qchunks, 1);
+        dpf_internal::ParallelChunks(nq, qchunks, [&](int c, int64_t lo, int64_t hi) {
+          for (int64_t j = std::max<int64_t>(lo, 1); j < hi; ++j)
+            if (q[j] < q[j - 1]) {
+              q_ok[c] = 0;
+              return;
+            }
+        });
+        sorted = std::all_of(q_ok.begin(), q_ok.end(), [](char x) { return x != 0; });
+      }
       std::unordered_map<uint128, int32_t, U128Hash> pos;
       if (!sorted) {
         pos.reserve(q.size() * 2);
@@ -728,12 +735,14 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   if (P > 0) {
     if (update_ctx) {
       std::swap(ctx.partial_prefixes_, tree_indices);
+      ctx.partial_sorted_ = indices_ascending;
       std::swap(ctx.seeds_, ctx.next_seeds_);
       std::swap(ctx.seeds_cap_, ctx.next_seeds_cap_);
       std::swap(ctx.ctrl_, ctx.next_ctrl_);
       std::swap(ctx.ctrl_cap_, ctx.next_ctrl_cap_);
     } else {
       ctx.partial_prefixes_.clear();
+      ctx.partial_sorted_ = false;
     }
     ctx.partial_evaluations_level_ = prev;
   }

@@ -565,6 +565,7 @@ PYBIND11_MODULE(_dpf_host, m) {
           d["outputs_per_level"] = r.outputs_per_level;
           d["key_size_bytes"] = r.key_size_bytes;
           d["seconds_per_iteration"] = r.seconds_per_iteration;
+          d["checksum_seconds_excluded"] = r.checksum_seconds;
           d["verified"] = r.verified;
           return d;
         },

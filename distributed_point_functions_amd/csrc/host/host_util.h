@@ -247,9 +247,13 @@ void ParallelChunks(int64_t n, int chunks, F fn) {
 // dedup (distributed_point_function.h:718-742).  Ascending prefixes (the
 // hierarchical case) take a two-pass parallel scan; anything else a hash map.
 // The output vectors are overwritten (their capacity is reused).
+// `*ascending_out` (if given) tells whether the tree indices came out strictly
+// ascending (ascending prefixes).
 inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<uint128>* tree_indices,
-                             std::vector<std::pair<int64_t, int>>* prefix_map) {
+                             std::vector<std::pair<int64_t, int>>* prefix_map,
+                             bool* ascending_out = nullptr) {
   const int64_t P = static_cast<int64_t>(prefixes.size());
+  if (ascending_out) *ascending_out = false;
   if (P == 0) {
     tree_indices->clear();
     prefix_map->clear();
@@ -257,27 +261,29 @@ inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<
   }
   const uint128 bmask = (static_cast<uint128>(1) << bib) - 1;
   const int chunks = NumChunks(P);
+  auto starts = [&](int64_t i) {
+    return i == 0 || (prefixes[i] >> bib) != (prefixes[i - 1] >> bib);
+  };
+  // One pass checks the order and counts each chunk's tree-index starts (the
+  // host side of a 1 M-prefix level is bound by memory traffic, config 5a).
   std::vector<char> chunk_ascending(chunks, 1);
+  std::vector<int64_t> first(chunks + 1, 0);
   ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
-    for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i)
+    int64_t k = lo == 0 ? 1 : 0;
+    for (int64_t i = std::max<int64_t>(lo, 1); i < hi; ++i) {
       if (!(prefixes[i - 1] < prefixes[i])) {
         chunk_ascending[c] = 0;
         return;
       }
+      k += starts(i);
+    }
+    first[c + 1] = k;
   });
   const bool ascending =
       std::all_of(chunk_ascending.begin(), chunk_ascending.end(), [](char a) { return a != 0; });
   if (ascending) {
-    // Equal tree indices are adjacent: count the starts per chunk, scan, place.
-    std::vector<int64_t> first(chunks + 1, 0);
-    auto starts = [&](int64_t i) {
-      return i == 0 || (prefixes[i] >> bib) != (prefixes[i - 1] >> bib);
-    };
-    ParallelChunks(P, chunks, [&](int c, int64_t lo, int64_t hi) {
-      int64_t k = 0;
-      for (int64_t i = lo; i < hi; ++i) k += starts(i);
-      first[c + 1] = k;
-    });
+    if (ascending_out) *ascending_out = true;
+    // Equal tree indices are adjacent: scan the starts per chunk, place.
     for (int c = 0; c < chunks; ++c) first[c + 1] += first[c];
     // Every element is overwritten below: vectors kept from an earlier call
     // (the caller's scratch) only value-initialise what they grow by.

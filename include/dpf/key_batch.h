@@ -161,6 +161,7 @@ class DeviceBatchContext {
   int previous_hierarchy_level_ = -1;
   int partial_evaluations_level_ = -1;
   std::vector<uint128> partial_prefixes_;
+  bool partial_sorted_ = false;  // partial_prefixes_ strictly ascending (skips a check)
   std::vector<uint128> spare_prefixes_;  // recycled storage for the next prefix list
   void* seeds_ = nullptr;  // current partial evaluations
   void* ctrl_ = nullptr;
