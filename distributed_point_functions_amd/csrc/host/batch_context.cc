@@ -334,9 +334,14 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   // kept from an earlier call of about this size value-initialise nothing
   // (clearing them had cost a 1 M-prefix level ~3.8 ms of single-threaded
   // zeroing, r16 DPF_BATCH_HOST_TIMING).
+  // Start nodes are indexed by int32 on the device (checked below), so 32-bit
+  // positions suffice: 8-byte (position, block index) entries.
+  if (P > INT32_MAX)
+    return ResourceExhaustedError(
+        "Too many start nodes for one batched evaluation; evaluate fewer levels at once.");
   std::vector<uint128> tree_indices = std::move(ctx.spare_prefixes_);
-  static thread_local std::vector<std::pair<int64_t, int>> tl_prefix_map;
-  std::vector<std::pair<int64_t, int>>& prefix_map = tl_prefix_map;
+  static thread_local std::vector<std::pair<int32_t, int>> tl_prefix_map;
+  std::vector<std::pair<int32_t, int>>& prefix_map = tl_prefix_map;
   bool indices_ascending = false;   // tree_indices strictly ascending
   if (P > 0) {
     dpf_internal::DedupTreeIndices(prefixes, prev_log - hierarchy_to_tree()[prev], &tree_indices,
@@ -354,6 +359,12 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   bool from_root = true;
   static thread_local std::vector<int32_t> tl_parent_of;   // recycled: no per-call zeroing
   std::vector<int32_t>& parent_of = tl_parent_of;
+  // Physical cache slot of each tree index's node (cached calls; see `cached`
+  // below), filled in the parent lookup's own pass when there is one.
+  static thread_local std::vector<int64_t> tl_start_slot;
+  std::vector<int64_t>& start_slot = tl_start_slot;
+  const bool g_cache_on = CacheOn();
+  bool slots_done = false;
   if (P == 0) {
     tree_indices.assign(1, 0);  // the root, expanded to depth Dh
   } else {
@@ -388,6 +399,14 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
       }
       parent_of.resize(tree_indices.size());
       const int64_t nt = static_cast<int64_t>(tree_indices.size());
+      // The same condition as `cached` below: the start slots come out of
+      // this pass (one read of tree_indices instead of two).
+      const int w1 = Dprev - start_level;
+      slots_done = g_cache_on && ctx.leaf_seeds_ && ctx.leaf_level_ == prev &&
+                   ctx.leaf_de_ == w1 && ctx.leaf_stride_ <= INT32_MAX;
+      if (slots_done) start_slot.resize(nt);
+      const uint128 slot_mask = slots_done ? (uint128{1} << w1) - 1 : 0;  // w1 <= 62 then
+      const std::vector<int32_t>& phys = ctx.leaf_phys_;
       std::atomic<int64_t> first_missing{nt};
       dpf_internal::ParallelFor(nt, [&](int64_t lo, int64_t hi) {
         size_t cursor = 0;  // merge pointer while the lookups ascend too
@@ -416,6 +435,10 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
             return;
           }
           parent_of[i] = static_cast<int32_t>(j);
+          if (slots_done) {
+            const int64_t logical = (j << w1) | static_cast<int64_t>(tree_indices[i] & slot_mask);
+            start_slot[i] = phys.empty() ? logical : phys[logical];
+          }
         }
       });
       if (first_missing.load() < nt)
@@ -446,7 +469,6 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   // partial evaluations stand for): the kernel reads their seeds from it and
   // the W1-level path walk is skipped.  Outputs and the
   // partial evaluations are the same either way.
-  const bool g_cache_on = CacheOn();
   const bool cached = g_cache_on && P > 0 && ctx.leaf_seeds_ && ctx.leaf_level_ == prev &&
                       ctx.leaf_de_ == W1 && ctx.leaf_stride_ <= INT32_MAX;
   const int Wk = cached ? 0 : W1;  // levels walked above each tree index
@@ -474,11 +496,8 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   bool swap_cache = false;
   bool gather = false;
   bool permute = false;
-  // Physical cache slot of each tree index's node (cached calls).
-  static thread_local std::vector<int64_t> tl_start_slot;
-  std::vector<int64_t>& start_slot = tl_start_slot;
   const uint128 leaf_mask = cached ? (uint128{1} << W1) - 1 : 0;  // W1 <= 62 when cached
-  if (cached) {
+  if (cached && !slots_done) {
     start_slot.resize(T);
     const std::vector<int32_t>& phys = ctx.leaf_phys_;
     dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
@@ -582,6 +601,15 @@ StatusOr<int64_t> DistributedPointFunction::EvaluateUntilBatchCore(
   dpf_block* path = need_path ? reinterpret_cast<dpf_block*>(img + off_path) : nullptr;
   const uint128 w1_mask = Wk >= 128 ? ~uint128{0} : ((uint128{1} << Wk) - 1);
   dpf_internal::ParallelFor(T, [&](int64_t lo, int64_t hi) {
+    if (!path && s == 0) {
+      // One start node per tree index and no walk (the cached steady state):
+      // the parents alone, without reading the tree indices.
+      for (int64_t i = lo; i < hi; ++i)
+        parent[i] = direct ? static_cast<int32_t>(start_slot[i])
+                    : gather ? static_cast<int32_t>(i)
+                             : (from_root ? 0 : parent_of[i]);
+      return;
+    }
     for (int64_t i = lo; i < hi; ++i) {
       const uint128 low = tree_indices[i] & w1_mask;
       // Cached: the physical cache slot of tree index i.

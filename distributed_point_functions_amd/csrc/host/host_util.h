@@ -249,9 +249,11 @@ void ParallelChunks(int64_t n, int chunks, F fn) {
 // The output vectors are overwritten (their capacity is reused).
 // `*ascending_out` (if given) tells whether the tree indices came out strictly
 // ascending (ascending prefixes).
-inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<uint128>* tree_indices,
-                             std::vector<std::pair<int64_t, int>>* prefix_map,
-                             bool* ascending_out = nullptr) {
+// `Pos` is the position type of prefix_map (int32_t halves its memory traffic
+// where the caller bounds the tree indices below 2^31).
+template <typename Pos>
+void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<uint128>* tree_indices,
+                      std::vector<std::pair<Pos, int>>* prefix_map, bool* ascending_out = nullptr) {
   const int64_t P = static_cast<int64_t>(prefixes.size());
   if (ascending_out) *ascending_out = false;
   if (P == 0) {
@@ -293,7 +295,7 @@ inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<
       int64_t pos = first[c] - 1;
       for (int64_t i = lo; i < hi; ++i) {
         if (starts(i)) (*tree_indices)[++pos] = prefixes[i] >> bib;
-        (*prefix_map)[i] = {pos, static_cast<int>(prefixes[i] & bmask)};
+        (*prefix_map)[i] = {static_cast<Pos>(pos), static_cast<int>(prefixes[i] & bmask)};
       }
     });
     return;
@@ -308,7 +310,7 @@ inline void DedupTreeIndices(Span<const uint128> prefixes, int bib, std::vector<
     const uint128 ti = prefixes[i] >> bib;
     auto [it, inserted] = inverse.try_emplace(ti, static_cast<int64_t>(tree_indices->size()));
     if (inserted) tree_indices->push_back(ti);
-    prefix_map->emplace_back(it->second, static_cast<int>(prefixes[i] & bmask));
+    prefix_map->emplace_back(static_cast<Pos>(it->second), static_cast<int>(prefixes[i] & bmask));
   }
 }
 
