@@ -288,8 +288,10 @@ class PartialEvaluation {
   DPF_PROTO_MESSAGE_API(PartialEvaluation)
 
  private:
-  bool has_prefix_ = false, has_seed_ = false;
+  // The flags after the two blocks: 40 bytes per element instead of 48 (a
+  // context holds ~1 M of these per level in config 5a, rewritten per call).
   Block prefix_, seed_;
+  bool has_prefix_ = false, has_seed_ = false;
   bool control_bit_ = false;
 };
 
