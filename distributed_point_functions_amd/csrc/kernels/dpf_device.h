@@ -245,6 +245,10 @@ struct ExpandParams {
   const uint8_t* cw_right;
   char* out;
   RoundKeys rkl, rkr, rkv, rkd;
+  // Octet kernel only: 0 = item u on thread u (grid stride); > 0 = workgroup b
+  // owns items [b, b + 1) * dyn_chunks * 64 and its waves take them 64 at a
+  // time from an LDS counter (dynamic distribution, dpf_kernels.hip).
+  int dyn_chunks;
   // Clock probe (dpf_hip_clock_probe): NULL, or [shader clocks, 100 MHz ticks,
   // workgroups] that wave 0 of every workgroup adds its s_memtime /
   // s_memrealtime deltas around its work into.  Nothing reads it back in the
@@ -259,21 +263,24 @@ struct ExpandParams {
 #ifndef DPF_CLOCK_PROBE
 #define DPF_CLOCK_PROBE 1   // 0: stamps compiled out (A/B variant builds)
 #endif
+#ifndef DPF_CLOCK_PROBE_WAVE
+#define DPF_CLOCK_PROBE_WAVE 0   // the stamped wave of each workgroup (variant builds: the last)
+#endif
 struct ClockStamp {
   unsigned long long c0 = 0, r0 = 0;
   __device__ __forceinline__ void begin(const unsigned long long* acc) {
-    if (DPF_CLOCK_PROBE && acc != nullptr && threadIdx.x < 64) {
+    if (DPF_CLOCK_PROBE && acc != nullptr && (threadIdx.x >> 6) == DPF_CLOCK_PROBE_WAVE) {
       c0 = __builtin_amdgcn_s_memtime();
       r0 = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) before the LDS loop
     }
   }
   __device__ __forceinline__ void end(unsigned long long* acc) {
-    if (DPF_CLOCK_PROBE && acc != nullptr && threadIdx.x < 64) {
+    if (DPF_CLOCK_PROBE && acc != nullptr && (threadIdx.x >> 6) == DPF_CLOCK_PROBE_WAVE) {
       const unsigned long long c1 = __builtin_amdgcn_s_memtime();
       const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_waitcnt(0xC07F);
-      if (threadIdx.x == 0) {
+      if ((threadIdx.x & 63) == 0) {
         atomicAdd(acc + 0, c1 - c0);
         atomicAdd(acc + 1, r1 - r0);
         atomicAdd(acc + 2, 1ull);

@@ -275,11 +275,13 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
   constexpr int kStash = OctetStash<Leaf>::value;
   __shared__ uint4 stash[kStash >= 1 ? kBlock : 1];
   __shared__ uint3 stash2[kStash >= 2 ? kBlock : 1];
+  __shared__ int next_chunk;   // dynamic distribution: the workgroup's next 64 items
   static_assert(sizeof(LdsImage) + (kStash >= 1 ? 16 * kBlock : 0) +
-                    (kStash >= 2 ? 12 * kBlock : 0) <= 160 * 1024, "LDS over 160 KiB");
+                    (kStash >= 2 ? 12 * kBlock : 0) + 16 <= 160 * 1024, "LDS over 160 KiB");
   leaf.init();
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
   const int k0 = p.k0, S = p.S;
@@ -287,8 +289,24 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_octet_kernel(Exp
   const int64_t ngroups = (int64_t)1 << G;
   ClockStamp stamp;
   stamp.begin(p.clock);
-  for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
-       item += (int64_t)gridDim.x * blockDim.x) {
+  // Items: thread u takes u, u + threads, ... (static), or -- dyn_chunks > 0
+  // -- each wave takes the workgroup's next 64 items from next_chunk until
+  // its range is used up.  The CU's arbiter favours its oldest waves (in
+  // config 2 wave 0 of a workgroup finished in 7.8 ms, wave 15 in 16.6 ms of
+  // a 16.9 ms launch): with a fixed share the last third of a launch runs on
+  // fewer and fewer waves, while taken dynamically the fast waves do more
+  // and all finish together.  Every lane of a wave holds the same chunk, so
+  // the DFS stays wave-uniform.
+  const int lane = (int)(threadIdx.x & 63);
+  auto take = [&]() -> int64_t {
+    int c = 0;
+    if (lane == 0) c = atomicAdd(&next_chunk, 1);
+    c = __builtin_amdgcn_readfirstlane(c);
+    return c < p.dyn_chunks ? ((int64_t)blockIdx.x * p.dyn_chunks + c) * 64 + lane : p.num_items;
+  };
+  for (int64_t item = p.dyn_chunks ? take() : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       item < p.num_items;
+       item = p.dyn_chunks ? take() : item + (int64_t)gridDim.x * blockDim.x) {
     // 1. walk from the start seed to this item's subtree root.
     const int64_t r = item >> k0;
     Block4 s = load_block(p.seeds_in + r);
@@ -923,6 +941,44 @@ int expand_top(ExpandParams& p, hipStream_t s, TopScratch& scratch) {
   return kOk;
 }
 
+// Dynamic item distribution for the octet kernel (ExpandParams::dyn_chunks):
+// a launch with at least 4 items per thread of one full workgroup per CU
+// gets subtrees two levels shallower (4x the items, the two levels above
+// them done by the tree-top pass) so every wave can take several chunks of
+// 64 items from its workgroup's counter.  Applied only when the tree-top
+// pass starts the items (k0 = 0 after it): otherwise every item would walk
+// two more levels.  DPF_OCTET_DYNAMIC=0 (read per launch) keeps the static
+// one-item-per-thread shape (A/B and test hook).
+bool octet_dynamic_on() {
+  const char* v = std::getenv("DPF_OCTET_DYNAMIC");
+  return !(v && v[0] == '0');
+}
+// Runs the tree-top pass and sets p's shape (and *grid, *blk) for the octet
+// kernel launch.
+int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int* blk) {
+  p.dyn_chunks = 0;
+  const int64_t cus = num_cus();
+  if (octet_dynamic_on() && p.S - 2 >= 3 && p.k0 + 2 <= 62 &&
+      (p.num_items << 2) % (cus * 64) == 0 && (p.num_items << 2) >= 4 * cus * kBlock) {
+    ExpandParams q = p;
+    q.S -= 2;
+    q.k0 += 2;
+    q.num_items <<= 2;
+    q.dyn_chunks = (int)(q.num_items / (cus * 64));
+    if (int st = expand_top(q, s, top)) return st;
+    if (q.k0 == 0) {
+      p = q;
+      *grid = (int)cus;
+      *blk = kBlock;
+      return kOk;
+    }
+  }
+  if (int st = expand_top(p, s, top)) return st;
+  *blk = block_for(p.num_items);
+  *grid = grid_for(p.num_items, *blk);
+  return kOk;
+}
+
 // The octet kernel takes integer leaves filling whole blocks whenever the
 // subtrees have >= 8 leaves (DPF_EXPAND_NO_OCTET=1 forces expand_kernel).
 template <int BITS, bool XOR>
@@ -933,10 +989,10 @@ bool launch_octet(const ExpandParams& p0, const dpf_block* vcw, int E, int party
   note_expand<FastIntLeaf<BITS, XOR>>(p0, true);
   ExpandParams p = p0;
   TopScratch top;
-  if ((*st = expand_top(p, s, top)) != kOk) return true;
-  const int blk = block_for(p.num_items);
-  hipLaunchKernelGGL((expand_octet_kernel<FastIntLeaf<BITS, XOR>>), dim3(grid_for(p.num_items, blk)),
-                     dim3(blk), 0, s, p, FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
+  int grid = 0, blk = 0;
+  if ((*st = octet_shape(p, s, top, &grid, &blk)) != kOk) return true;
+  hipLaunchKernelGGL((expand_octet_kernel<FastIntLeaf<BITS, XOR>>), dim3(grid), dim3(blk), 0, s, p,
+                     FastIntLeaf<BITS, XOR>{vcw, E, party, store_bytes, {}});
   return true;
 }
 
@@ -2057,6 +2113,7 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
   if (num_levels >= DPF_FORCE_S) S = DPF_FORCE_S;  // variant builds (tools/variant_bench.py)
 #endif
   ExpandParams p;
+  p.dyn_chunks = 0;
   p.num_levels = num_levels;
   p.S = S;
   p.k0 = num_levels - S;
@@ -2128,10 +2185,9 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
       if (p.S >= 3 && !(off_env && off_env[0] == '1')) {
         note_expand<SwarLeaf>(p, true);
         TopScratch top;
-        if (int st = expand_top(p, s, top)) return st;
-        const int blk = block_for(p.num_items);
-        hipLaunchKernelGGL((expand_octet_kernel<SwarLeaf>), dim3(grid_for(p.num_items, blk)),
-                           dim3(blk), 0, s, p, w);
+        int grid = 0, blk = 0;
+        if (int st = octet_shape(p, s, top, &grid, &blk)) return st;
+        hipLaunchKernelGGL((expand_octet_kernel<SwarLeaf>), dim3(grid), dim3(blk), 0, s, p, w);
         HIP_TRY(hipGetLastError());
         return kOk;
       }
@@ -2161,10 +2217,9 @@ int dpf_hip_expand(int64_t num_starts, const dpf_block* seeds_in, const uint8_t*
         // Octet form (the half's four leaves hashed as two ILP4 groups).
         note_expand<Mod32Leaf<2>>(p, true);
         TopScratch top;
-        if (int st = expand_top(p, s, top)) return st;
-        const int blk = block_for(p.num_items);
-        hipLaunchKernelGGL((expand_octet_kernel<Mod32Leaf<2>>), dim3(grid_for(p.num_items, blk)),
-                           dim3(blk), 0, s, p, m);
+        int grid = 0, blk = 0;
+        if (int st = octet_shape(p, s, top, &grid, &blk)) return st;
+        hipLaunchKernelGGL((expand_octet_kernel<Mod32Leaf<2>>), dim3(grid), dim3(blk), 0, s, p, m);
         HIP_TRY(hipGetLastError());
         return kOk;
       }
