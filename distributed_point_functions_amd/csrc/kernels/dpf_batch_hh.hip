@@ -382,6 +382,8 @@ struct HHKeysParams {
   int64_t u_ranges;     // start-node ranges per 64-key group
   int64_t u_per_range;
   int64_t num_waves;    // ceil(K / 64) * u_ranges
+  unsigned int* task_counter;  // non-NULL: waves take tasks one at a time from this
+                               // zeroed counter (dynamic); NULL: grid stride
   int cw_level;
   int cw_stride;
   int nl;
@@ -514,7 +516,19 @@ void hh_keys_kernel(HHKeysParams p) {
                         __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nl = p.nl;
   const Div32 div0 = p.div[0], div1 = p.div[1];
-  for (int64_t w = wave0; w < p.num_waves; w += (int64_t)gridDim.x * waves_per_block) {
+  // Tasks (64 keys x a range of start nodes) by grid stride, or -- with a
+  // task counter -- taken one at a time in order, so the waves the CU's
+  // arbiter favours take more of them and all finish together (the octet
+  // kernel's items, dpf_kernels.hip; the LDS here is full, so the counter is
+  // in global memory).  Neighbouring tasks share their 64 keys.
+  auto take = [&]() -> int64_t {
+    unsigned int c = 0;
+    if (lane == 0) c = atomicAdd(p.task_counter, 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    return (int64_t)c < p.num_waves ? (int64_t)c : p.num_waves;
+  };
+  for (int64_t w = p.task_counter ? take() : wave0; w < p.num_waves;
+       w = p.task_counter ? take() : w + (int64_t)gridDim.x * waves_per_block) {
     const int64_t grp = w / p.u_ranges;
     const int64_t rng = w - grp * p.u_ranges;
     const int64_t k_raw = grp * 64 + lane;
@@ -706,9 +720,12 @@ int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
   p.num_keys = a.num_keys;
   p.num_starts = a.num_starts;
   const int64_t groups = (a.num_keys + 63) / 64;
-  // At least ~4 waves per wave slot of the chip: split the start nodes when
-  // there are few 64-key groups.
-  const int64_t want_waves = (int64_t)num_cus() * (kHHKeysBlock / 64) * 4;
+  // At least ~4 tasks per wave slot of the chip (16 when they are taken
+  // dynamically, DPF_HH_DYNAMIC=0 turns that off): split the start nodes
+  // when there are few 64-key groups.
+  const char* dyn_env = std::getenv("DPF_HH_DYNAMIC");
+  const bool dynamic = !(dyn_env && dyn_env[0] == '0');
+  const int64_t want_waves = (int64_t)num_cus() * (kHHKeysBlock / 64) * (dynamic ? 16 : 4);
   int64_t ranges = (want_waves + groups - 1) / groups;
   if (ranges > a.num_starts) ranges = a.num_starts;
   if (ranges < 1) ranges = 1;
@@ -742,6 +759,7 @@ int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
   int64_t grid = (p.num_waves * 64 + kHHKeysBlock - 1) / kHHKeysBlock;
   if (grid > num_cus()) grid = num_cus();   // one 128 KiB-table workgroup per CU
   if (grid < 1) grid = 1;
+  if (p.num_waves > (int64_t)UINT32_MAX / 2) return fail(kInvalidArgument, "too many tasks");
   void* tab = nullptr;
   if (DPF_HH_KEYS_MODE == 2) {
     // Stream-ordered scratch (48 B per key), freed behind the kernel; the
@@ -755,13 +773,21 @@ int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
       return hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep) == hipSuccess;
     }();
     (void)pool_kept;
-    HIP_TRY(hipMallocAsync(&tab, (size_t)a.num_keys * 3 * sizeof(uint4), s));
+    // The key table, then the dynamic task counter.
+    HIP_TRY(hipMallocAsync(&tab, (size_t)a.num_keys * 3 * sizeof(uint4) + 256, s));
     int64_t g = (a.num_keys + 255) / 256;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(hh_key_table_kernel, dim3((unsigned)g), dim3(256), 0, s, a.num_keys,
                        a.cw_level, a.cw_stride, a.cw_seed, a.cw_left, a.cw_right, a.vcw,
                        a.vcw_stride, a.nl, a.party, static_cast<uint4*>(tab));
     p.key_tab = static_cast<const uint4*>(tab);
+  } else {
+    HIP_TRY(hipMallocAsync(&tab, 256, s));
+  }
+  if (dynamic) {
+    p.task_counter = reinterpret_cast<unsigned int*>(
+        static_cast<char*>(tab) + (DPF_HH_KEYS_MODE == 2 ? (size_t)a.num_keys * 3 * sizeof(uint4) : 0));
+    HIP_TRY(hipMemsetAsync(p.task_counter, 0, sizeof(unsigned int), s));
   }
   hipLaunchKernelGGL(hh_keys_kernel, dim3((unsigned)grid), dim3(kHHKeysBlock), 0, s, p);
   const hipError_t e = hipGetLastError();

@@ -948,22 +948,26 @@ int expand_top(ExpandParams& p, hipStream_t s, TopScratch& scratch) {
 // 64 items from its workgroup's counter.  Applied only when the tree-top
 // pass starts the items (k0 = 0 after it): otherwise every item would walk
 // two more levels.  DPF_OCTET_DYNAMIC=0 (read per launch) keeps the static
-// one-item-per-thread shape (A/B and test hook).
-bool octet_dynamic_on() {
+// one-item-per-thread shape, =<1..4> sets the levels taken off the subtrees
+// (2^that items per thread; A/B and test hook).
+int octet_dynamic_shift() {
   const char* v = std::getenv("DPF_OCTET_DYNAMIC");
-  return !(v && v[0] == '0');
+  if (!v || !*v) return 2;
+  const int k = std::atoi(v);
+  return k <= 0 ? 0 : (k > 4 ? 4 : k);
 }
 // Runs the tree-top pass and sets p's shape (and *grid, *blk) for the octet
 // kernel launch.
 int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int* blk) {
   p.dyn_chunks = 0;
   const int64_t cus = num_cus();
-  if (octet_dynamic_on() && p.S - 2 >= 3 && p.k0 + 2 <= 62 &&
-      (p.num_items << 2) % (cus * 64) == 0 && (p.num_items << 2) >= 4 * cus * kBlock) {
+  const int sh = octet_dynamic_shift();
+  if (sh > 0 && p.S - sh >= 3 && p.k0 + sh <= 62 &&
+      (p.num_items << sh) % (cus * 64) == 0 && (p.num_items << sh) >= 4 * cus * kBlock) {
     ExpandParams q = p;
-    q.S -= 2;
-    q.k0 += 2;
-    q.num_items <<= 2;
+    q.S -= sh;
+    q.k0 += sh;
+    q.num_items <<= sh;
     q.dyn_chunks = (int)(q.num_items / (cus * 64));
     if (int st = expand_top(q, s, top)) return st;
     if (q.k0 == 0) {
