@@ -173,6 +173,7 @@ struct DcfFastParams {
   const uint8_t* cw_right;
   char* out;
   RoundKeys rkl, rkd, rkv;
+  int64_t dyn_per_wg;  // dcf_fast_kernel: take_chunk's per_wg (0: grid stride)
 };
 
 struct DcfVcw {
@@ -183,13 +184,21 @@ template <int BITS, bool XOR, bool UNIFORM, int ITEMS>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_fast_kernel(DcfFastParams p,
                                                                          DcfVcw vc) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h)
   fill_tables(lds.tab);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int n = p.n;
   using Acc = typename std::conditional<BITS == 128, u128, uint64_t>::type;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; (g >> 6) < p.num_groups;
-       g += (int64_t)gridDim.x * blockDim.x) {
+  // Groups of 64 lanes by grid stride, or taken one at a time per wave
+  // (dyn_per_wg > 0).
+  const int64_t done = p.num_groups * 64;
+  for (int64_t g = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, p.num_groups, done)
+                                : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       (g >> 6) < p.num_groups;
+       g = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, p.num_groups, done)
+                        : g + (int64_t)gridDim.x * blockDim.x) {
     const int64_t base = (g >> 6) * (64 * ITEMS) + (g & 63);
     int64_t u[ITEMS], k[ITEMS];
     bool valid[ITEMS];
@@ -378,6 +387,8 @@ void launch_dcf_fast(const DcfFastParams& p0, const DcfVcw& vc, hipStream_t s) {
   p.num_groups = (p.num_items + 63) / 64;
   const int blk = block_for(p.num_groups * 64);
   const dim3 grid(grid_for(p.num_groups * 64, blk)), block(blk);
+  // DPF_DCF_DYNAMIC=0: a fixed share of groups per thread (A/B hook).
+  p.dyn_per_wg = dynamic_chunks_per_wg(p.num_groups * 64, (int)grid.x, blk, "DPF_DCF_DYNAMIC");
   if (p.points_per_key % 64 == 0)
     hipLaunchKernelGGL((dcf_fast_kernel<BITS, XOR, true, 1>), grid, block, 0, s, p, vc);
   else

@@ -256,6 +256,25 @@ struct ExpandParams {
   unsigned long long* clock;
 };
 
+// Dynamic distribution of 64-item chunks over a workgroup's waves (r16).
+// A CU's arbiter favours its oldest waves, so with a fixed share per thread
+// the first waves of a workgroup finish long before the last (config 2's
+// octet kernel: wave 0 at 7.8 ms, wave 15 at 16.6 ms of a 16.9 ms launch) and
+// the end of every launch runs on fewer and fewer waves.  Taken one chunk
+// at a time instead, the favoured waves do more of the work and all finish
+// together.  Workgroup b owns chunks [b * per_wg, (b + 1) * per_wg) below
+// `chunks`; the wave's lane 0 takes the next from `counter` (LDS, zeroed
+// before the workgroup's first take).  Returns chunk * 64 + lane, or `done`
+// once the workgroup's chunks are used up; wave-uniform.
+__device__ __forceinline__ int64_t take_chunk(int* counter, int64_t per_wg, int64_t chunks,
+                                              int64_t done) {
+  int c = 0;
+  if ((threadIdx.x & 63) == 0) c = atomicAdd(counter, 1);
+  c = __builtin_amdgcn_readfirstlane(c);
+  const int64_t g = (int64_t)blockIdx.x * per_wg + c;
+  return c < per_wg && g < chunks ? g * 64 + (int64_t)(threadIdx.x & 63) : done;
+}
+
 // Stamps of the clock probe: wave-uniform (wave 0 of the workgroup), two
 // reads per workgroup, so the probe costs nothing measurable in a launch of
 // milliseconds (MI355X_MICROARCH.md: in-kernel clock = delta s_memtime /

@@ -432,6 +432,7 @@ struct PointParams {
   int esz;
   int xor_mode;               // fast leaves: XorWrapper
   RoundKeys rkl, rkd, rkv;
+  int64_t dyn_per_wg;         // eval_points4_kernel: take_chunk's per_wg (0: grid stride)
 };
 
 // Latency mode of full-domain expansion for small trees (r15; config 1 and
@@ -756,6 +757,14 @@ int block_for(int64_t work_items) {
   return (int)b;
 }
 
+int64_t dynamic_chunks_per_wg(int64_t items, int grid, int block, const char* env) {
+  const char* v = env ? std::getenv(env) : nullptr;
+  if (v && v[0] == '0') return 0;
+  const int64_t chunks = (items + 63) / 64;
+  if (chunks < (int64_t)grid * (block / 64) * 4) return 0;
+  return (chunks + grid - 1) / grid;
+}
+
 int grid_for(int64_t work_items, int block) {
   int64_t g = (work_items + block - 1) / block;
   int64_t cap = num_cus() * kWgPerCu;  // one 128 KiB-LDS workgroup per CU
@@ -1027,15 +1036,22 @@ int launch_expand_fast(const ExpandParams& p, const dpf_value_desc* d, const dpf
 template <int BITS, bool UNIFORM, bool SUM>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(PointParams p) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h)
   fill_tables(lds.tab);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int L = p.num_levels;
   const int64_t P = p.points_per_key, quarter = p.half;
   // Sums of <= 64-bit values wrap mod 2^64 exactly (the group is mod 2^BITS).
   using Acc = typename std::conditional<(BITS <= 64), uint64_t, u128>::type;
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
-       u += (int64_t)gridDim.x * blockDim.x) {
+  // Items by grid stride, or 64 at a time per wave (dyn_per_wg > 0).
+  const int64_t nch = (p.num_items + 63) / 64;
+  for (int64_t u = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.num_items)
+                                : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       u < p.num_items;
+       u = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.num_items)
+                        : u + (int64_t)gridDim.x * blockDim.x) {
     int64_t grp = u / quarter;
     if (UNIFORM) grp = (int64_t)__builtin_amdgcn_readfirstlane((int)grp);
     const int64_t q0 = u - grp * quarter;
@@ -1213,8 +1229,10 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
       p.half = quarter;
       p.num_items = items;
       const int blk = block_for(p.num_items);
-      hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM>), dim3(grid_for(p.num_items, blk)),
-                         dim3(blk), 0, s, p);
+      const int grid = grid_for(p.num_items, blk);
+      // DPF_POINTS_DYNAMIC=0: a fixed share of items per thread (A/B hook).
+      p.dyn_per_wg = dynamic_chunks_per_wg(p.num_items, grid, blk, "DPF_POINTS_DYNAMIC");
+      hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM>), dim3(grid), dim3(blk), 0, s, p);
       HIP_TRY(hipGetLastError());
       return kOk;
     }
@@ -1319,6 +1337,7 @@ int make_point_params(int64_t num_keys, int64_t points_per_key, int num_levels,
   p->vcw_stride = desc->elements_per_block * desc->num_leaves;
   p->esz = packed_size(desc);
   p->xor_mode = desc->kind[0] == DPF_LEAF_XOR;
+  p->dyn_per_wg = 0;
   p->rkl = expand_key(key_left);
   p->rkd = xor_keys(p->rkl, expand_key(key_right));
   p->rkv = expand_key(key_value);

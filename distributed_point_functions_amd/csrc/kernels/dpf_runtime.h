@@ -22,6 +22,10 @@ int num_cus();                                 // compute units of the current d
 int block_for(int64_t work_items);             // threads per workgroup: kBlock, or fewer
                                                // (multiple of 64) to spread a small launch over more CUs
 int grid_for(int64_t work_items, int block);   // workgroups of `block` threads, <= one per CU
+// Chunks of 64 items per workgroup for take_chunk (dpf_device.h), or 0 (a
+// fixed share per thread): dynamic when the launch gives every wave at least
+// 4 chunks and `env` is not "0" (A/B and test hooks, read per launch).
+int64_t dynamic_chunks_per_wg(int64_t items, int grid, int block, const char* env);
 int validate_desc(const dpf_value_desc* d);    // kOk or the failure code
 int packed_size(const dpf_value_desc* d);      // bytes of one packed element
 bool fast_int(const dpf_value_desc* d);        // one plain/XOR integer leaf, direct, b == 1
