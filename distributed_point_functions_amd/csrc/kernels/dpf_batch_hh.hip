@@ -723,9 +723,11 @@ int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
   // At least ~4 tasks per wave slot of the chip (16 when they are taken
   // dynamically, DPF_HH_DYNAMIC=0 turns that off): split the start nodes
   // when there are few 64-key groups.
+  // DPF_HH_DYNAMIC=<n>: n tasks per wave slot (A/B hook).
   const char* dyn_env = std::getenv("DPF_HH_DYNAMIC");
-  const bool dynamic = !(dyn_env && dyn_env[0] == '0');
-  const int64_t want_waves = (int64_t)num_cus() * (kHHKeysBlock / 64) * (dynamic ? 16 : 4);
+  const int per_slot = dyn_env && *dyn_env ? std::atoi(dyn_env) : 16;
+  const bool dynamic = per_slot > 0;
+  const int64_t want_waves = (int64_t)num_cus() * (kHHKeysBlock / 64) * (dynamic ? per_slot : 4);
   int64_t ranges = (want_waves + groups - 1) / groups;
   if (ranges > a.num_starts) ranges = a.num_starts;
   if (ranges < 1) ranges = 1;

@@ -2342,8 +2342,11 @@ int dpf_hip_eval_points_sum(int64_t num_keys, int64_t num_points, int num_levels
   const size_t wide_bytes = (size_t)num_points * desc->num_leaves * 3 * sizeof(uint64_t);
   HIP_TRY(hipMemsetAsync(workspace, 0, wide_bytes, s));
   if (num_keys > 0) {
-    // Enough (chunk, pair) items to fill every CU's 1024 threads a few times.
-    const int64_t want = (int64_t)num_cus() * kBlock * 4;
+    // Enough (chunk, pair) items to fill every CU's 1024 threads a few times
+    // (16 times when the waves take them dynamically: enough chunks per wave
+    // for take_chunk; each item then sums fewer keys before its atomics).
+    const char* dyn = std::getenv("DPF_POINTS_DYNAMIC");
+    const int64_t want = (int64_t)num_cus() * kBlock * (dyn && dyn[0] == '0' ? 4 : 16);
     int64_t chunks = (want + p.half - 1) / p.half;
     if (chunks > num_keys) chunks = num_keys;
     p.chunk_keys = (num_keys + chunks - 1) / chunks;
