@@ -720,12 +720,13 @@ int launch_hh_keys(const HHLevelArgs& a, hipStream_t s) {
   p.num_keys = a.num_keys;
   p.num_starts = a.num_starts;
   const int64_t groups = (a.num_keys + 63) / 64;
-  // At least ~4 tasks per wave slot of the chip (16 when they are taken
-  // dynamically, DPF_HH_DYNAMIC=0 turns that off): split the start nodes
-  // when there are few 64-key groups.
+  // At least ~4 tasks per wave slot of the chip (64 when they are taken
+  // dynamically -- 2^20-client pass 17.16 / 16.71 / 16.39 / 16.28 s at 8 /
+  // 16 / 32 / 64, profiles/r16/hh_dynamic_ab.txt; DPF_HH_DYNAMIC=0 turns that
+  // off): split the start nodes when there are few 64-key groups.
   // DPF_HH_DYNAMIC=<n>: n tasks per wave slot (A/B hook).
   const char* dyn_env = std::getenv("DPF_HH_DYNAMIC");
-  const int per_slot = dyn_env && *dyn_env ? std::atoi(dyn_env) : 16;
+  const int per_slot = dyn_env && *dyn_env ? std::atoi(dyn_env) : 64;
   const bool dynamic = per_slot > 0;
   const int64_t want_waves = (int64_t)num_cus() * (kHHKeysBlock / 64) * (dynamic ? per_slot : 4);
   int64_t ranges = (want_waves + groups - 1) / groups;
