@@ -64,12 +64,14 @@ LOG_PER_GPU = 30          # 2^30 uint64 outputs per GPU (BASELINE.json configs[1
 #  * LDS (`roofline_lds`, the bound of the T-table design): 160 conflict-free
 #    ds_read_b32 lookups = 640 B at 128 B/clk/CU -> 5 clk/block/CU -> 122.9 G.
 #  * measured LDS ceiling (`roofline_lds_measured`): conflict-free random
-#    ds_read_b32 lookups in this layout sustain 26.3 lanes/clk/CU, not 32
-#    (tools/lds_ceiling_microbench.hip, profiles/r11_lds_ceiling.txt) ->
-#    26.3 x 256 x 2.4 GHz / 160 = 101.0 G blocks/s at the nominal clock.
+#    ds_read_b32 lookups in this layout sustain 31.0 lanes/clk/CU of the 32
+#    when every wave takes its work in chunks (tools/lds_ceiling_microbench.hip,
+#    profiles/r16/lds_ceiling.txt; r11's 26.3 with fixed per-wave shares
+#    included the launch's staggered tail) -> 31.0 x 256 x 2.4 GHz / 160 =
+#    119.0 G blocks/s at the nominal clock.
 AES_VALU_PEAK_GBLOCKS = 245.8
 AES_LDS_PEAK_GBLOCKS = 122.9
-AES_LDS_MEASURED_GBLOCKS = 101.0
+AES_LDS_MEASURED_GBLOCKS = 119.0
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md
 METRIC = "DPF leaf evals/sec, full-domain 2^30 uint64 at 1/2/4/8 GPUs; AES blocks/s"
 KERNEL = "expand_octet_kernel<FastIntLeaf<64, false> >"
@@ -400,7 +402,7 @@ def aes_rooflines(achieved: float, kernel: str, **extra) -> dict:
         "roofline_lds_measured": {"bound": "lds, measured lookup ceiling", "achieved": achieved,
                                   "peak": AES_LDS_MEASURED_GBLOCKS, "unit": "G AES-128 blocks/s",
                                   "frac": achieved / AES_LDS_MEASURED_GBLOCKS,
-                                  "source": "profiles/r11_lds_ceiling.txt (2.4 GHz nominal)"},
+                                  "source": "profiles/r16/lds_ceiling.txt (2.4 GHz nominal)"},
     }
 
 
