@@ -958,10 +958,14 @@ int expand_top(ExpandParams& p, hipStream_t s, TopScratch& scratch) {
 // pass starts the items (k0 = 0 after it): otherwise every item would walk
 // two more levels.  DPF_OCTET_DYNAMIC=0 (read per launch) keeps the static
 // one-item-per-thread shape, =<1..4> sets the levels taken off the subtrees
-// (2^that items per thread; A/B and test hook).
-int octet_dynamic_shift() {
+// (2^that items per thread; A/B and test hook).  Default: 4 levels off
+// subtrees of >= 11 (config 2 15.00 vs 15.05-15.17 ms, config 3's uint128
+// shard 58.2 vs 60.9 ms, Tuple<IntModN32 x 2> 39.2 vs 40.9 ms), else 2 (the
+// 2^27 / 2^28 shards 1.96 / 3.82 ms at 2 vs 2.04 / 3.90 at 4; 3 was worse than
+// both everywhere; profiles/r16/octet_dynamic_ab.txt).
+int octet_dynamic_shift(int S) {
   const char* v = std::getenv("DPF_OCTET_DYNAMIC");
-  if (!v || !*v) return 2;
+  if (!v || !*v) return S >= 11 ? 4 : 2;
   const int k = std::atoi(v);
   return k <= 0 ? 0 : (k > 4 ? 4 : k);
 }
@@ -970,7 +974,7 @@ int octet_dynamic_shift() {
 int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int* blk) {
   p.dyn_chunks = 0;
   const int64_t cus = num_cus();
-  const int sh = octet_dynamic_shift();
+  const int sh = octet_dynamic_shift(p.S);
   if (sh > 0 && p.S - sh >= 3 && p.k0 + sh <= 62 &&
       (p.num_items << sh) % (cus * 64) == 0 && (p.num_items << sh) >= 4 * cus * kBlock) {
     ExpandParams q = p;
