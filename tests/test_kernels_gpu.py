@@ -361,3 +361,35 @@ def test_eval_points_pairing_threshold(hip, vt, ppk):
 def test_eval_points_shapes(hip, vt, num_keys, ppk, levels, partials):
     _points_case(hip, np.random.default_rng(ppk * 31 + levels), vt, num_keys, ppk, levels,
                  from_partials=partials)
+
+
+# Dynamic distribution in the octet kernel (dpf_kernels.hip octet_shape):
+# launches with >= 4 items per thread of the chip take 2 or 4 levels off the
+# subtrees and let each wave take 64 items at a time from its workgroup's
+# counter.  At 2^26 leaves both shapes apply; every shape must give the
+# static one-item-per-thread launch's bytes (DPF_OCTET_DYNAMIC=0), which the
+# tests above and the full-size tests tie to the oracle.
+@pytest.mark.parametrize("vt", [("int", 64), ("tuple", [("intmodn", 32, M32)] * 2),
+                                ("tuple", [("int", 32), ("int", 64)])], ids=str)
+def test_expand_octet_dynamic_shapes(hip, vt, monkeypatch):
+    import torch
+    rng = np.random.default_rng(hash((str(vt), "dyn")) & 0xFFFFFFFF)
+    levels, party = 26, 1
+    b = (O.bits_needed(vt, 40.0) + 127) // 128
+    E = O.elements_per_block(vt)
+    args = (hip.to_device_blocks(_rand_blocks(rng, 1)),
+            hip.to_device_u8(rng.integers(0, 2, size=1, dtype=np.uint8)),
+            hip.to_device_blocks(_rand_blocks(rng, levels)),
+            hip.to_device_u8(rng.integers(0, 2, size=levels, dtype=np.uint8)),
+            hip.to_device_u8(rng.integers(0, 2, size=levels, dtype=np.uint8)),
+            (O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE), _desc(hip, vt, b), E,
+            hip.to_device_blocks(O._leaf_array([_rand_value(rng, vt) for _ in range(E)])), party)
+    monkeypatch.setenv("DPF_OCTET_DYNAMIC", "0")
+    want = hip.expand(*args)
+    assert hip.last_expand_kernel()[0].startswith("octet/")
+    for mode in ("2", "4", ""):
+        monkeypatch.setenv("DPF_OCTET_DYNAMIC", mode)
+        got = hip.expand(*args)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), mode
+        del got
