@@ -969,6 +969,14 @@ int octet_dynamic_shift(int S) {
   const int k = std::atoi(v);
   return k <= 0 ? 0 : (k > 4 ? 4 : k);
 }
+// Levels each dynamically taken item walks below the tree-top pass's roots
+// (DPF_OCTET_WALK=<n>, read per launch; 0: the pass goes down to the items).
+int octet_walk_levels() {
+  const char* v = std::getenv("DPF_OCTET_WALK");
+  if (!v || !*v) return 2;
+  const int k = std::atoi(v);
+  return k < 0 ? 0 : (k > 4 ? 4 : k);
+}
 // Runs the tree-top pass and sets p's shape (and *grid, *blk) for the octet
 // kernel launch.
 int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int* blk) {
@@ -982,6 +990,31 @@ int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int*
     q.k0 += sh;
     q.num_items <<= sh;
     q.dyn_chunks = (int)(q.num_items / (cus * 64));
+    // The tree-top pass stops `w` levels above the items (a quarter of the
+    // roots for w = 2: fewer rounds of its latency-bound workgroups), and
+    // every item walks those levels itself (one path step per level, in the
+    // octet kernel's throughput mode).
+    const int w = octet_walk_levels();
+    if (w > 0 && q.k0 - w >= 8) {
+      ExpandParams t = q;
+      t.k0 = q.k0 - w;
+      t.S = q.S + w;
+      t.num_items = q.num_items >> w;
+      if (int st = expand_top(t, s, top)) return st;
+      if (t.k0 == 0) {
+        q.seeds_in = t.seeds_in;
+        q.ctrl_in = t.ctrl_in;
+        q.cw_seed = t.cw_seed;
+        q.cw_left = t.cw_left;
+        q.cw_right = t.cw_right;
+        q.num_levels = q.S + w;
+        q.k0 = w;
+        p = q;
+        *grid = (int)cus;
+        *blk = kBlock;
+        return kOk;
+      }
+    }
     if (int st = expand_top(q, s, top)) return st;
     if (q.k0 == 0) {
       p = q;
