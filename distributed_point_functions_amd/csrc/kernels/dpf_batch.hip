@@ -56,6 +56,7 @@ struct BatchLevelParams {
   int64_t chunk_keys;
   int64_t waves_per_chunk;  // ceil(U / 64)
   int64_t num_threads;      // num_chunks * waves_per_chunk * 64
+  int64_t dyn_per_wg;       // take_chunk's per_wg (0: grid stride)
   int walk_levels;
   int save_after;           // -1: no partial evaluations are stored
   int expand_levels;        // <= kMaxExpand
@@ -454,15 +455,23 @@ template <class V, int MAXE, bool SUM>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void batch_level_kernel(
     BatchLevelParams p, V v) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h)
   fill_tables(lds.tab);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(
       lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
   const int64_t U = p.num_starts;
   const int W = p.walk_levels;
   const int NL = 1 << p.expand_levels;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.num_threads;
-       g += (int64_t)gridDim.x * blockDim.x) {
+  // Wave tasks (key chunk x 64 start nodes) by grid stride, or taken one at a
+  // time per wave (dyn_per_wg > 0).
+  const int64_t tasks = p.num_threads >> 6;
+  for (int64_t g = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, tasks, p.num_threads)
+                                : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       g < p.num_threads;
+       g = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, tasks, p.num_threads)
+                        : g + (int64_t)gridDim.x * blockDim.x) {
     const int64_t wave = g >> 6;
     const int64_t chunk = (int64_t)__builtin_amdgcn_readfirstlane((int)(wave / p.waves_per_chunk));
     const int64_t u_raw = (wave - chunk * p.waves_per_chunk) * 64 + (g & 63);
@@ -664,10 +673,13 @@ __global__ void gather_batched_kernel(int64_t keys, int64_t in_row, int64_t rows
 }
 
 template <class V, int MAXE, bool SUM>
-int launch_batch(const BatchLevelParams& p, const V& v, hipStream_t s) {
+int launch_batch(const BatchLevelParams& p0, const V& v, hipStream_t s) {
+  BatchLevelParams p = p0;
   const int blk = block_for(p.num_threads);
-  hipLaunchKernelGGL((batch_level_kernel<V, MAXE, SUM>), dim3(grid_for(p.num_threads, blk)),
-                     dim3(blk), 0, s, p, v);
+  const int grid = grid_for(p.num_threads, blk);
+  // DPF_BATCH_DYNAMIC=0: a fixed share of wave tasks per wave (A/B hook).
+  p.dyn_per_wg = dynamic_chunks_per_wg(p.num_threads, grid, blk, "DPF_BATCH_DYNAMIC");
+  hipLaunchKernelGGL((batch_level_kernel<V, MAXE, SUM>), dim3(grid), dim3(blk), 0, s, p, v);
   HIP_TRY(hipGetLastError());
   return kOk;
 }
@@ -873,7 +885,9 @@ int dpf_hip_eval_prefix_batch_layout(
     p.num_keys = num_keys;
     p.num_starts = num_starts;
     p.waves_per_chunk = (num_starts + 63) / 64;
-    const int64_t want_waves = (int64_t)num_cus() * (kBlock / 64) * 4;
+    // ~4 wave tasks per wave slot, 16 when they are taken dynamically.
+    const char* dyn = std::getenv("DPF_BATCH_DYNAMIC");
+    const int64_t want_waves = (int64_t)num_cus() * (kBlock / 64) * (dyn && dyn[0] == '0' ? 4 : 16);
     int64_t chunks = (want_waves + p.waves_per_chunk - 1) / p.waves_per_chunk;
     if (chunks > num_keys) chunks = num_keys;
     if (chunks < 1) chunks = 1;
