@@ -118,17 +118,25 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_paths_kernel(PathP
 template <class Leaf>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void expand_kernel(ExpandParams p, Leaf leaf) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h), p.dyn_chunks > 0
   leaf.init();
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), key_ref(p.rkr), key_ref(p.rkv), key_ref(p.rkd)});
   const int k0 = p.k0, S = p.S;
   const int B = S >= 1 ? 1 : 0;  // leaf pairs share their parent
   const int G = S - B;            // depth of the DFS stack
   const int64_t ngroups = (int64_t)1 << G;
-  for (int64_t item = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; item < p.num_items;
-       item += (int64_t)gridDim.x * blockDim.x) {
+  // Items by grid stride, or 64 at a time per wave (dyn_chunks > 0, as the
+  // octet kernel).
+  const int64_t nch = (p.num_items + 63) / 64;
+  for (int64_t item = p.dyn_chunks ? take_chunk(&next_chunk, p.dyn_chunks, nch, p.num_items)
+                                   : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       item < p.num_items;
+       item = p.dyn_chunks ? take_chunk(&next_chunk, p.dyn_chunks, nch, p.num_items)
+                           : item + (int64_t)gridDim.x * blockDim.x) {
     // 1. walk from the start seed to this item's subtree root.
     const int64_t r = item >> k0;
     Block4 s = load_block(p.seeds_in + r);
@@ -862,21 +870,6 @@ bool try_small(const ExpandParams& p0, const Leaf& leaf, hipStream_t s) {
   return true;
 }
 
-template <class Leaf>
-int launch_expand(const ExpandParams& p, const Leaf& leaf, hipStream_t s) {
-  // GenericLeaf's conversion spills in the small kernel's register budget and
-  // measured 0.93-1.07x there (profiles/r15_ab.txt part 13): not dispatched.
-  if (!std::is_same_v<Leaf, GenericLeaf> && try_small(p, leaf, s)) {
-    HIP_TRY(hipGetLastError());
-    return kOk;
-  }
-  note_expand<Leaf>(p, false);
-  const int blk = block_for(p.num_items);
-  hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid_for(p.num_items, blk)), dim3(blk), 0, s, p,
-                     leaf);
-  HIP_TRY(hipGetLastError());
-  return kOk;
-}
 
 // Tree-top pass of an octet launch (r16).  Every octet-kernel item walks k0
 // levels from its start seed to its subtree root, one dependent AES per level
@@ -979,11 +972,12 @@ int octet_walk_levels() {
 }
 // Runs the tree-top pass and sets p's shape (and *grid, *blk) for the octet
 // kernel launch.
-int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int* blk) {
+int subtree_shape(ExpandParams& p, int min_S, hipStream_t s, TopScratch& top, int* grid,
+                  int* blk) {
   p.dyn_chunks = 0;
   const int64_t cus = num_cus();
   const int sh = octet_dynamic_shift(p.S);
-  if (sh > 0 && p.S - sh >= 3 && p.k0 + sh <= 62 &&
+  if (sh > 0 && p.S - sh >= min_S && p.k0 + sh <= 62 &&
       (p.num_items << sh) % (cus * 64) == 0 && (p.num_items << sh) >= 4 * cus * kBlock) {
     ExpandParams q = p;
     q.S -= sh;
@@ -1026,6 +1020,29 @@ int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int*
   if (int st = expand_top(p, s, top)) return st;
   *blk = block_for(p.num_items);
   *grid = grid_for(p.num_items, *blk);
+  return kOk;
+}
+int octet_shape(ExpandParams& p, hipStream_t s, TopScratch& top, int* grid, int* blk) {
+  return subtree_shape(p, 3, s, top, grid, blk);
+}
+
+template <class Leaf>
+int launch_expand(const ExpandParams& p0, const Leaf& leaf, hipStream_t s) {
+  // GenericLeaf's conversion spills in the small kernel's register budget and
+  // measured 0.93-1.07x there (profiles/r15_ab.txt part 13): not dispatched.
+  if (!std::is_same_v<Leaf, GenericLeaf> && try_small(p0, leaf, s)) {
+    HIP_TRY(hipGetLastError());
+    return kOk;
+  }
+  note_expand<Leaf>(p0, false);
+  // The octet kernel's shape (tree-top pass, dynamic 64-item chunks) with
+  // pair leaves: subtrees of >= 1 level.
+  ExpandParams p = p0;
+  TopScratch top;
+  int grid = 0, blk = 0;
+  if (int st = subtree_shape(p, 1, s, top, &grid, &blk)) return st;
+  hipLaunchKernelGGL(expand_kernel<Leaf>, dim3(grid), dim3(blk), 0, s, p, leaf);
+  HIP_TRY(hipGetLastError());
   return kOk;
 }
 

@@ -393,3 +393,34 @@ def test_expand_octet_dynamic_shapes(hip, vt, monkeypatch):
         torch.cuda.synchronize()
         assert torch.equal(got, want), mode
         del got
+
+
+# The pair-leaf kernel (expand_kernel: GenericLeaf types and DPF_EXPAND_NO_OCTET)
+# takes the same dynamic shape (tree-top pass, 64-item chunks per wave); at
+# 2^24 leaves every mode equals the static launch byte for byte.
+@pytest.mark.parametrize("vt", [("int", 64), ("tuple", [("intmodn", 64, M64)] * 2)], ids=str)
+def test_expand_pair_dynamic_shapes(hip, vt, monkeypatch):
+    import torch
+    rng = np.random.default_rng(hash((str(vt), "pairdyn")) & 0xFFFFFFFF)
+    levels, party = 24, 0
+    b = (O.bits_needed(vt, 40.0) + 127) // 128
+    E = O.elements_per_block(vt)
+    args = (hip.to_device_blocks(_rand_blocks(rng, 1)),
+            hip.to_device_u8(rng.integers(0, 2, size=1, dtype=np.uint8)),
+            hip.to_device_blocks(_rand_blocks(rng, levels)),
+            hip.to_device_u8(rng.integers(0, 2, size=levels, dtype=np.uint8)),
+            hip.to_device_u8(rng.integers(0, 2, size=levels, dtype=np.uint8)),
+            (O.PRG_KEY_LEFT, O.PRG_KEY_RIGHT, O.PRG_KEY_VALUE), _desc(hip, vt, b), E,
+            hip.to_device_blocks(O._leaf_array([_rand_value(rng, vt) for _ in range(E)])), party)
+    monkeypatch.setenv("DPF_EXPAND_NO_OCTET", "1")
+    monkeypatch.setenv("DPF_OCTET_DYNAMIC", "0")
+    monkeypatch.setenv("DPF_EXPAND_TOP", "0")
+    want = hip.expand(*args)
+    assert hip.last_expand_kernel()[0].startswith("pair/")
+    monkeypatch.delenv("DPF_EXPAND_TOP")
+    for mode in ("0", "2", "4", ""):
+        monkeypatch.setenv("DPF_OCTET_DYNAMIC", mode)
+        got = hip.expand(*args)
+        torch.cuda.synchronize()
+        assert torch.equal(got, want), mode
+        del got
