@@ -48,6 +48,7 @@ struct DcfParams {
   const uint8_t* cw_right;
   char* out;
   RoundKeys rkl, rkd, rkv;
+  int64_t dyn_per_wg;  // take_chunk's per_wg (0: grid stride)
 };
 
 __device__ __forceinline__ u128 shr128(u128 x, int s) { return s >= 128 ? (u128)0 : x >> s; }
@@ -56,13 +57,20 @@ template <int BITS, bool FAST>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void dcf_eval_kernel(
     DcfParams p, DcfLevels lv, GenericLeaf g) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h)
   fill_tables(lds.tab);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int n = lv.n;
   const int dmax = lv.depth[n - 1];
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
-       u += (int64_t)gridDim.x * blockDim.x) {
+  // Items by grid stride, or 64 at a time per wave (dyn_per_wg > 0).
+  const int64_t nch = (p.num_items + 63) / 64;
+  for (int64_t u = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.num_items)
+                                : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       u < p.num_items;
+       u = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.num_items)
+                        : u + (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = u / p.points_per_key, j = u - k * p.points_per_key;
     const u128 x = dpf_u128(p.points[p.shared_points ? j : u]);
     const int party = p.party[k] & 1;
@@ -504,6 +512,7 @@ extern "C" int dpf_hip_dcf_eval_batch(int64_t num_keys, int64_t points_per_key, 
   }
   const int blk = block_for(items);
   const dim3 grid(grid_for(items, blk)), block(blk);
+  p.dyn_per_wg = dynamic_chunks_per_wg(items, (int)grid.x, blk, "DPF_DCF_DYNAMIC");
   if (fast) {
     switch (desc->bits[0]) {
       case 8: hipLaunchKernelGGL((dcf_eval_kernel<8, true>), grid, block, 0, s, p, lv, g); break;

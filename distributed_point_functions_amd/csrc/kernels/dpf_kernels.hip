@@ -580,13 +580,21 @@ struct SeedLeaf {
 template <class Leaf, int BITS, bool FAST, bool UNIFORM, bool SUM, bool PAIRED = true>
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points_kernel(PointParams p, Leaf leaf) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h)
   fill_tables(lds.tab);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, key_ref(p.rkv), key_ref(p.rkd)});
   const int L = p.num_levels;
   const int64_t P = p.points_per_key, half = p.half;
-  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < p.num_items;
-       u += (int64_t)gridDim.x * blockDim.x) {
+  // Items by grid stride, or 64 at a time per wave (dyn_per_wg > 0; a chunk
+  // cut off by num_items is the range's last, after which no lane takes more).
+  const int64_t nch = (p.num_items + 63) / 64;
+  for (int64_t u = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.num_items)
+                                : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       u < p.num_items;
+       u = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.num_items)
+                        : u + (int64_t)gridDim.x * blockDim.x) {
     int64_t grp = u / half;
     if (UNIFORM) grp = (int64_t)__builtin_amdgcn_readfirstlane((int)grp);
     const int64_t q0 = u - grp * half;
@@ -1323,9 +1331,10 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
     }
   }
   g_last_points_kernel = "points/ilp2";
-  const PointParams& p = pp;
+  PointParams p = pp;
   const int blk = block_for(p.num_items);
   const dim3 grid(grid_for(p.num_items, blk)), block(blk);
+  p.dyn_per_wg = dynamic_chunks_per_wg(p.num_items, (int)grid.x, blk, "DPF_POINTS_DYNAMIC");
   if (p.half % 64 == 0)
     hipLaunchKernelGGL((eval_points_kernel<Leaf, BITS, FAST, true, SUM>), grid, block, 0, s, p, leaf);
   else

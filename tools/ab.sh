@@ -7,7 +7,8 @@
 # A variant is
 #   lib:<name>        vlib/<name>.so copied over the in-tree libdpf_hip.so
 #                     (built by tools/build_variant.sh), restored afterwards;
-#   env:<VAR>=<val>   the current library with that environment variable set;
+#   env:<VAR>=<val>[,<VAR>=<val>...]   the current library with those
+#                     environment variables set;
 #   cur               the current library, no extra environment.
 # Usage (GPU box, repo root):
 #   bash tools/ab.sh [--tests "tests/a.py tests/b.py"] [--rounds N] [--tag t] \
@@ -39,11 +40,11 @@ for r in $(seq 1 $ROUNDS); do
     envset=""
     case $v in
       lib:*) cp vlib/${v#lib:}.so $L ;;
-      env:*) envset=${v#env:} ;;
+      env:*) envset=${v#env:}; envset=${envset//,/ } ;;
       cur) ;;
       *) echo "ab.sh: bad variant $v"; restore; exit 2 ;;
     esac
-    log=$O/${TAG}_$(echo $v | tr ':=/' '___')_r$r.log
+    log=$O/${TAG}_$(echo $v | tr ':=/,' '____')_r$r.log
     env $envset timeout -k 10 600 python bench.py $ARGS --no-cpu-baseline > $log 2>&1
     rc=$?; restore
     [ $rc -eq 0 ] || { echo "$v failed"; tail -5 $log; exit 1; }
