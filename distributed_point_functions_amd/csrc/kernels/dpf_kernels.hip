@@ -68,14 +68,20 @@ namespace {
 
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void hash_kernel(int64_t n, const dpf_block* __restrict__ in,
                                                       dpf_block* __restrict__ out,
-                                                      RoundKeys rk) {
+                                                      RoundKeys rk, int64_t dyn_per_wg) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h); dyn_per_wg 0: grid stride
   fill_tables(lds.tab);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   const KeyRef kr = key_ref(rk);
   LdsLookup lk = make_lookup(lds, KeySet{kr, kr, kr, kr});
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t nch = (n + 63) / 64;
+  for (int64_t i = dyn_per_wg ? take_chunk(&next_chunk, dyn_per_wg, nch, n)
+                              : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       i < n;
+       i = dyn_per_wg ? take_chunk(&next_chunk, dyn_per_wg, nch, n)
+                      : i + (int64_t)gridDim.x * blockDim.x) {
     store_block(out + i, dpf_aes::mmo_hash(load_block(in + i), lk, UniformRK{lk.ks.v}));
   }
 }
@@ -92,17 +98,24 @@ struct PathParams {
   dpf_block* seeds_out;
   uint8_t* ctrl_out;
   RoundKeys rkl, rkd;
+  int64_t dyn_per_wg;  // take_chunk's per_wg (0: grid stride)
 };
 
 
 __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_paths_kernel(PathParams p) {
   __shared__ LdsImage lds;
+  __shared__ int next_chunk;   // take_chunk (dpf_device.h)
   fill_tables(lds.tab);
   fill_cws(lds, p.cw_seed, p.cw_left, p.cw_right, p.num_levels);
+  if (threadIdx.x == 0) next_chunk = 0;
   __syncthreads();
   LdsLookup lk = make_lookup(lds, KeySet{key_ref(p.rkl), KeyRef{}, KeyRef{}, key_ref(p.rkd)});
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p.n;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t nch = (p.n + 63) / 64;
+  for (int64_t i = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.n)
+                                : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       i < p.n;
+       i = p.dyn_per_wg ? take_chunk(&next_chunk, p.dyn_per_wg, nch, p.n)
+                        : i + (int64_t)gridDim.x * blockDim.x) {
     Block4 s = load_block(p.seeds_in + i);
     uint32_t t = p.ctrl_in[i] & 1u;
     Block4 path = load_block(p.paths + i);
@@ -2107,8 +2120,10 @@ int dpf_hip_hash(int64_t n, const dpf_block* in, const dpf_aes_key* key, dpf_blo
   if (n == 0) return kOk;
   if (!in || !out || !key) return fail(kInvalidArgument, "NULL pointer");
   const int blk = block_for(n);
-  hipLaunchKernelGGL(hash_kernel, dim3(grid_for(n, blk)), dim3(blk), 0, (hipStream_t)stream, n,
-                     in, out, expand_key(key));
+  const int grid = grid_for(n, blk);
+  // DPF_HASH_DYNAMIC=0: a fixed share of blocks per thread (A/B hook).
+  hipLaunchKernelGGL(hash_kernel, dim3(grid), dim3(blk), 0, (hipStream_t)stream, n, in, out,
+                     expand_key(key), dynamic_chunks_per_wg(n, grid, blk, "DPF_HASH_DYNAMIC"));
   HIP_TRY(hipGetLastError());
   return kOk;
 }
@@ -2147,7 +2162,9 @@ int dpf_hip_eval_paths(int64_t num_seeds, int num_levels, const dpf_block* seeds
   p.rkl = expand_key(key_left);
   p.rkd = xor_keys(p.rkl, expand_key(key_right));
   const int blk = block_for(num_seeds);
-  hipLaunchKernelGGL(eval_paths_kernel, dim3(grid_for(num_seeds, blk)), dim3(blk), 0, s, p);
+  const int grid = grid_for(num_seeds, blk);
+  p.dyn_per_wg = dynamic_chunks_per_wg(num_seeds, grid, blk, "DPF_PATHS_DYNAMIC");
+  hipLaunchKernelGGL(eval_paths_kernel, dim3(grid), dim3(blk), 0, s, p);
   HIP_TRY(hipGetLastError());
   return kOk;
 }

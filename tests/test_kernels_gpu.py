@@ -86,6 +86,46 @@ def test_eval_paths_matches_reference_grid(hip, num_seeds, num_levels):
     np.testing.assert_array_equal(c.cpu().numpy(), want_c)
 
 
+@pytest.mark.parametrize("dynamic", ["1", "0"])
+def test_hash_and_paths_full_launch(hip, dynamic, monkeypatch):
+    """Launches large enough for dynamic 64-item chunks per wave (2^21 + a
+    ragged tail) and, with DPF_HASH_DYNAMIC=0 / DPF_PATHS_DYNAMIC=0, the fixed
+    grid-stride share: sampled rows (first, last, random) equal the oracle and
+    the two distributions agree on every row."""
+    import torch
+    rng = np.random.default_rng(21)
+    n = (1 << 21) + 5
+    x = _rand_blocks(rng, n)
+    d = hip.to_device_blocks(x)
+    rows = np.unique(np.concatenate([[0, 63, 64, n - 1], rng.integers(0, n, size=512)]))
+    got = {}
+    for dyn in (dynamic, "1" if dynamic == "0" else "0"):
+        monkeypatch.setenv("DPF_HASH_DYNAMIC", dyn)
+        got[dyn] = hip.blocks_to_numpy(hip.hash_blocks(d, O.PRG_KEY_LEFT))
+    np.testing.assert_array_equal(got["1"], got["0"])
+    np.testing.assert_array_equal(got[dynamic][rows], O.aes_hash(O.PRG_KEY_LEFT, x[rows]))
+    levels = 20
+    paths = _rand_blocks(rng, n)
+    ctrl = rng.integers(0, 2, size=n, dtype=np.uint8)
+    cws = _rand_blocks(rng, levels)
+    cl = rng.integers(0, 2, size=levels, dtype=np.uint8)
+    cr = rng.integers(0, 2, size=levels, dtype=np.uint8)
+    dev = [hip.to_device_blocks(x), hip.to_device_u8(ctrl), hip.to_device_blocks(paths),
+           hip.to_device_blocks(cws), hip.to_device_u8(cl), hip.to_device_u8(cr)]
+    res = {}
+    for dyn in ("1", "0"):
+        monkeypatch.setenv("DPF_PATHS_DYNAMIC", dyn)
+        s, c = hip.eval_paths(*dev, KEY0, KEY1)
+        torch.cuda.synchronize()
+        res[dyn] = (hip.blocks_to_numpy(s), c.cpu().numpy())
+    np.testing.assert_array_equal(res["1"][0], res["0"][0])
+    np.testing.assert_array_equal(res["1"][1], res["0"][1])
+    want_s, want_c = O.evaluate_seeds(x[rows[:64]], ctrl[rows[:64]], paths[rows[:64]], cws, cl, cr,
+                                      KEY0, KEY1)
+    np.testing.assert_array_equal(res[dynamic][0][rows[:64]], want_s)
+    np.testing.assert_array_equal(res[dynamic][1][rows[:64]], want_c)
+
+
 def _desc(hip, vt, b):
     return hip.value_desc(O.leaves(vt), O.is_direct(vt), O.elements_per_block(vt), b)
 
