@@ -454,6 +454,7 @@ struct PointParams {
   int xor_mode;               // fast leaves: XorWrapper
   RoundKeys rkl, rkd, rkv;
   int64_t dyn_per_wg;         // eval_points4_kernel: take_chunk's per_wg (0: grid stride)
+  int top_levels;             // eval_points4_kernel: 0 or 6 levels walked once per wave
 };
 
 // Latency mode of full-domain expansion for small trees (r15; config 1 and
@@ -1163,7 +1164,43 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(Poi
       const dpf_block* cws = p.cw_seed + k * p.cw_stride;
       const uint8_t* cl = p.cw_left + k * p.cw_stride;
       const uint8_t* cr = p.cw_right + k * p.cw_stride;
-      for (int j = 0; j < L; ++j) {
+      // Shared top (top_levels = 6, walks from the root): the wave's 256
+      // points of this key share its top 6 levels, so lane l walks them once
+      // for the prefix whose 6 path bits are l (one AES per level instead of
+      // four), and each chain takes its depth-6 node from the lane its own
+      // top bits name (ds_bpermute, no LDS allocation).
+      const int j0 = p.top_levels;
+      if (j0) {
+        const uint32_t lane = threadIdx.x & 63;
+        Block4 ts = st[0];
+        uint32_t tt = t[0];
+        for (int j = 0; j < j0; ++j) {
+          const dpf_block c = cws[j];
+          const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
+          const uint32_t b = (lane >> (j0 - 1 - j)) & 1u;
+          Block4 h = dpf_aes::mmo_hash(ts, lk, SelectRK{lk.ks.l, lk.ks.d, 0u - b});
+          const uint32_t m = 0u - tt;
+          h.w0 ^= (uint32_t)c.low & m;
+          h.w1 ^= (uint32_t)(c.low >> 32) & m;
+          h.w2 ^= (uint32_t)c.high & m;
+          h.w3 ^= (uint32_t)(c.high >> 32) & m;
+          tt = (h.w0 & 1u) ^ (tt & ((cctl >> b) & 1u));
+          h.w0 &= ~1u;
+          ts = h;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t src = 0;
+          for (int j = 0; j < j0; ++j) src = (src << 1) | path_bit(path[i], L - 1 - j + p.bib);
+          const int a = (int)(src << 2);
+          st[i] = Block4{(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)ts.w0),
+                         (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)ts.w1),
+                         (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)ts.w2),
+                         (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)ts.w3)};
+          t[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)tt);
+        }
+      }
+      for (int j = j0; j < L; ++j) {
         const dpf_block c = cws[j];
         const uint32_t cctl = (uint32_t)(cl[j] & 1) | ((uint32_t)(cr[j] & 1) << 1);
         uint32_t b[4];
@@ -1307,6 +1344,9 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
       const int grid = grid_for(p.num_items, blk);
       // DPF_POINTS_DYNAMIC=0: a fixed share of items per thread (A/B hook).
       p.dyn_per_wg = dynamic_chunks_per_wg(p.num_items, grid, blk, "DPF_POINTS_DYNAMIC");
+      // DPF_POINTS_SHARED_TOP=0: every chain walks the whole path (A/B hook).
+      const char* top = std::getenv("DPF_POINTS_SHARED_TOP");
+      p.top_levels = !p.seeds_in && p.num_levels >= 6 && !(top && top[0] == '0') ? 6 : 0;
       hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM>), dim3(grid), dim3(blk), 0, s, p);
       HIP_TRY(hipGetLastError());
       return kOk;
@@ -1414,6 +1454,7 @@ int make_point_params(int64_t num_keys, int64_t points_per_key, int num_levels,
   p->esz = packed_size(desc);
   p->xor_mode = desc->kind[0] == DPF_LEAF_XOR;
   p->dyn_per_wg = 0;
+  p->top_levels = 0;
   p->rkl = expand_key(key_left);
   p->rkd = xor_keys(p->rkl, expand_key(key_right));
   p->rkv = expand_key(key_value);

@@ -182,19 +182,25 @@ ILP_CASES = [
     ([(64, ("xor", 128), 0)], 3, 256),
     ([(30, ("int", 8), 0)], 4, 256),                 # 16 elements per block
     ([(10, ("int", 16), 0), (50, ("int", 64), 0)], 4, 256),
+    ([(7, ("int", 64), 0)], 2, 256),                 # 6 tree levels: all shared
+    ([(6, ("int", 64), 0)], 2, 256),                 # 5: no shared top
 ]
 
 
-@pytest.mark.parametrize("ilp", ["4", "2"])
+@pytest.mark.parametrize("ilp", ["4", "4/full-walk", "2"])
 @pytest.mark.parametrize("levels,n_keys,ppk", ILP_CASES, ids=str)
 def test_points_kernel_chains_per_lane(levels, n_keys, ppk, ilp, monkeypatch):
     """Integer point evaluation with four path chains per lane
-    (eval_points4_kernel, the default for launches that fill the chip) and with
-    two (eval_points_kernel), forced through DPF_POINTS_ILP: per-key points,
-    shared points and the key sum all equal the oracle, and the dispatch
-    diagnostic names the kernel that ran."""
+    (eval_points4_kernel, the default for launches that fill the chip; its top
+    6 levels walked once per wave, or with DPF_POINTS_SHARED_TOP=0 by every
+    chain) and with two (eval_points_kernel), forced through DPF_POINTS_ILP:
+    per-key points, shared points and the key sum all equal the oracle, and the
+    dispatch diagnostic names the kernel that ran."""
     import torch
     from distributed_point_functions_amd import hip_abi as H
+    if ilp.endswith("/full-walk"):
+        ilp = ilp.split("/")[0]
+        monkeypatch.setenv("DPF_POINTS_SHARED_TOP", "0")
     monkeypatch.setenv("DPF_POINTS_ILP", ilp)
     h = len(levels) - 1
     dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=ppk + int(ilp))
