@@ -187,20 +187,20 @@ ILP_CASES = [
 ]
 
 
-@pytest.mark.parametrize("ilp", ["4", "4/full-walk", "2"])
+@pytest.mark.parametrize("ilp", ["4", "4/full-walk", "4/shared-top", "2"])
 @pytest.mark.parametrize("levels,n_keys,ppk", ILP_CASES, ids=str)
 def test_points_kernel_chains_per_lane(levels, n_keys, ppk, ilp, monkeypatch):
     """Integer point evaluation with four path chains per lane
     (eval_points4_kernel, the default for launches that fill the chip; its top
-    6 levels walked once per wave, or with DPF_POINTS_SHARED_TOP=0 by every
-    chain) and with two (eval_points_kernel), forced through DPF_POINTS_ILP:
+    6 levels walked once per wave by default in the key sum, forced on or off
+    for both forms with DPF_POINTS_SHARED_TOP=1|0) and with two (eval_points_kernel), forced through DPF_POINTS_ILP:
     per-key points, shared points and the key sum all equal the oracle, and the
     dispatch diagnostic names the kernel that ran."""
     import torch
     from distributed_point_functions_amd import hip_abi as H
-    if ilp.endswith("/full-walk"):
-        ilp = ilp.split("/")[0]
-        monkeypatch.setenv("DPF_POINTS_SHARED_TOP", "0")
+    if "/" in ilp:
+        ilp, walk = ilp.split("/")
+        monkeypatch.setenv("DPF_POINTS_SHARED_TOP", "1" if walk == "shared-top" else "0")
     monkeypatch.setenv("DPF_POINTS_ILP", ilp)
     h = len(levels) - 1
     dpf, P, rng, batch, oks, _, _, _ = _setup(levels, n_keys, seed=ppk + int(ilp))
