@@ -89,6 +89,7 @@ struct HHParams {
   const int32_t* leaf_slot;  // NULL: leaf i of start node u at slot (u << 2) + i
   Div32 div[2];
   RoundKeys rkl, rkr, rkv;
+  unsigned int* task_counter;  // non-NULL: waves take their 64-thread tasks from this
 };
 
 // value = sampled IntModN elements of one leaf (value_type_helpers.h:286-311):
@@ -206,8 +207,18 @@ void hh_level_kernel(HHParams p) {
   for (int e = 0; e < 2; ++e)
     div[e] = Div32{pin_sgpr(p.div[e].dn), pin_sgpr(p.div[e].v), (int)pin_sgpr((uint32_t)p.div[e].sh),
                    pin_sgpr(p.div[e].n)};
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.num_threads;
-       g += (int64_t)gridDim.x * blockDim.x) {
+  // Tasks (64 threads each) by grid stride, or one at a time per wave from
+  // the global counter (task_counter, as hh_keys_kernel).
+  const int64_t num_tasks = p.num_threads >> 6;
+  auto next = [&](int64_t g) -> int64_t {
+    if (!p.task_counter) return g + (int64_t)gridDim.x * blockDim.x;
+    unsigned int c = 0;
+    if ((threadIdx.x & 63) == 0) c = atomicAdd(p.task_counter, 1u);
+    c = __builtin_amdgcn_readfirstlane(c);
+    return (int64_t)c < num_tasks ? (int64_t)c * 64 + (threadIdx.x & 63) : p.num_threads;
+  };
+  for (int64_t g = p.task_counter ? next(0) : blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+       g < p.num_threads; g = next(g)) {
     const int64_t wave = g >> 6;
     const int64_t chunk = (int64_t)__builtin_amdgcn_readfirstlane((int)(wave / p.waves_per_chunk));
     const int64_t u_raw = (wave - chunk * p.waves_per_chunk) * 64 + (g & 63);
@@ -808,7 +819,12 @@ int launch_hh_level(const HHLevelArgs& a, hipStream_t s) {
   p.num_keys = a.num_keys;
   p.num_starts = a.num_starts;
   p.waves_per_chunk = (a.num_starts + 63) / 64;
-  const int64_t want_waves = (int64_t)num_cus() * (kBlock / 64) * 4;
+  // ~4 tasks per wave slot, or DPF_HH_DYNAMIC (default 64) taken dynamically
+  // (0: the fixed grid-stride share).
+  const char* dyn_env = std::getenv("DPF_HH_DYNAMIC");
+  const int per_slot = dyn_env && *dyn_env ? std::atoi(dyn_env) : 64;
+  const bool dynamic = per_slot > 0;
+  const int64_t want_waves = (int64_t)num_cus() * (kBlock / 64) * (dynamic ? per_slot : 4);
   int64_t chunks = (want_waves + p.waves_per_chunk - 1) / p.waves_per_chunk;
   if (chunks > a.num_keys) chunks = a.num_keys;
   if (chunks < 1) chunks = 1;
@@ -845,8 +861,16 @@ int launch_hh_level(const HHLevelArgs& a, hipStream_t s) {
   int64_t grid = (p.num_threads + kHHBlock - 1) / kHHBlock;
   if (grid > num_cus()) grid = num_cus();   // one 128 KiB-LDS workgroup per CU
   if (grid < 1) grid = 1;
+  void* counter = nullptr;
+  if (dynamic) {
+    HIP_TRY(hipMallocAsync(&counter, 256, s));
+    HIP_TRY(hipMemsetAsync(counter, 0, sizeof(unsigned int), s));
+    p.task_counter = static_cast<unsigned int*>(counter);
+  }
   hipLaunchKernelGGL(hh_level_kernel, dim3((unsigned)grid), dim3(kHHBlock), 0, s, p);
-  HIP_TRY(hipGetLastError());
+  const hipError_t e = hipGetLastError();
+  if (counter) HIP_TRY(hipFreeAsync(counter, s));
+  HIP_TRY(e);
   return kOk;
 }
 
