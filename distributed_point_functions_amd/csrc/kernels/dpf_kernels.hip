@@ -454,7 +454,7 @@ struct PointParams {
   int xor_mode;               // fast leaves: XorWrapper
   RoundKeys rkl, rkd, rkv;
   int64_t dyn_per_wg;         // eval_points4_kernel: take_chunk's per_wg (0: grid stride)
-  int top_levels;             // eval_points4_kernel: 0 or 6 (TOP) levels walked once per wave
+  int top_levels;             // eval_points4_kernel: nonzero: the TOP instance (6 / 4 levels walked once per wave)
 };
 
 // Latency mode of full-domain expansion for small trees (r15; config 1 and
@@ -1169,7 +1169,10 @@ __global__ __launch_bounds__(kBlock) DPF_WAVES_ATTR void eval_points4_kernel(Poi
       // for the prefix whose 6 path bits are l (one AES per level instead of
       // four), and each chain takes its depth-6 node from the lane its own
       // top bits name (ds_bpermute, no LDS allocation).
-      constexpr int j0 = TOP ? 6 : 0;
+      // 6 levels in the key sum; 4 per key, whose instance schedules its path
+      // loop as the full walk does only with the shorter top (ISA: 9 waits in
+      // the round block vs 40 with 6 levels).
+      constexpr int j0 = TOP ? (SUM ? 6 : 4) : 0;
       if (TOP) {
         const uint32_t lane = threadIdx.x & 63;
         Block4 ts = st[0];
@@ -1344,13 +1347,11 @@ int launch_points_t(const PointParams& pp, const Leaf& leaf, hipStream_t s) {
       const int grid = grid_for(p.num_items, blk);
       // DPF_POINTS_DYNAMIC=0: a fixed share of items per thread (A/B hook).
       p.dyn_per_wg = dynamic_chunks_per_wg(p.num_items, grid, blk, "DPF_POINTS_DYNAMIC");
-      // The shared top by default only where it measured faster: summed over
-      // keys 1236 vs 1275 ms, but per key 1358 vs 1258 ms (its per-key
-      // instance schedules the path loop worse, r16h in
-      // profiles/r16/points_shared_top_ab.txt).  DPF_POINTS_SHARED_TOP=0|1
-      // turns it off / on for both (A/B hook).
+      // The shared top (profiles/r16/points_shared_top_ab.txt): summed over
+      // keys 6 levels, 1236 vs 1275 ms; per key 4 levels (6 measured 1358 vs
+      // 1258 ms, r16h).  DPF_POINTS_SHARED_TOP=0 turns it off (A/B hook).
       const char* top = std::getenv("DPF_POINTS_SHARED_TOP");
-      const bool want_top = top && (top[0] == '0' || top[0] == '1') ? top[0] == '1' : SUM;
+      const bool want_top = !(top && top[0] == '0');
       p.top_levels = want_top && !p.seeds_in && p.num_levels >= 6 ? 6 : 0;
       if (p.top_levels)
         hipLaunchKernelGGL((eval_points4_kernel<BITS, true, SUM, true>), dim3(grid), dim3(blk), 0, s, p);
